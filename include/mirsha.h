@@ -1,0 +1,162 @@
+/*
+ * mirsha.h -- C ABI of the MI355X batched SHA-256 digest engine for MirBFT's
+ * hash path (libmirsha.so, built from mirbft_amd/csrc/).
+ *
+ * This is the drop-in boundary. In the reference, hashing is
+ *
+ *   processor.Hasher                 /root/reference/pkg/processor/serial.go:21-23
+ *       New() hash.Hash              (crypto.SHA256: mirbft_test.go:392, testengine/recorder.go:781)
+ *   processor.ProcessHashActions     /root/reference/pkg/processor/serial.go:180-198
+ *       (hasher, *ActionList) -> (*EventList, error)
+ *
+ * called once per accumulated ActionList from Node.doHashWork
+ * (/root/reference/mirbft.go:282-302) and from the testengine
+ * (/root/reference/pkg/testengine/recorder.go:604-610). A cgo adapter packs the
+ * ActionList's [][]byte parts into one arena (cgo forbids passing Go memory that
+ * holds Go pointers, so [][]byte cannot cross as-is) and makes ONE call below per
+ * list; see INTEGRATION.md for the binding.
+ *
+ * Conventions
+ *  - Every function returns MSHA_OK (0) or a positive MSHA_ERR_* code; nothing
+ *    throws or aborts across the ABI. msha_last_error() describes the last
+ *    failure on a context (or, for ctx == NULL, the last failure of
+ *    msha_ctx_create on this thread).
+ *  - Host pointers are owned by the caller and only used during the call; the
+ *    library copies into its own pinned staging and device memory and never
+ *    retains them. Digests are written to caller memory (32 bytes each, in input
+ *    order), so the caller can hand out fresh copies (the state machine keeps
+ *    digests as map keys: batch_tracker.go:85-91, epoch_change.go:42-50).
+ *  - A context is used by one thread at a time (the reference hashes on one
+ *    goroutine, mirbft.go:470); distinct contexts may be used concurrently.
+ *    Each call selects its device(s) explicitly, so OS-thread migration between
+ *    calls (goroutines) is harmless.
+ *  - There is no CPU fallback: with no usable GPU, msha_ctx_create fails with
+ *    MSHA_ERR_NO_DEVICE.
+ */
+#ifndef MIRSHA_H_
+#define MIRSHA_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MSHA_ABI_VERSION 1u
+
+enum {
+  MSHA_OK = 0,
+  MSHA_ERR_INVALID_ARG = 1, /* null pointer, range outside arena, bad bounds */
+  MSHA_ERR_NO_DEVICE = 2,   /* no GPU, or device_mask names a missing device */
+  MSHA_ERR_HIP = 3,         /* a HIP runtime call failed (message has details) */
+  MSHA_ERR_OUT_OF_MEMORY = 4,
+  MSHA_ERR_ALIGNMENT = 5    /* device-resident message not 16-byte aligned */
+};
+
+/* Bytes that must stay readable after the last message of a DEVICE arena
+ * passed to the *_device entry points (the kernels read a message's final
+ * block as one whole 64-byte block; bytes past each message are masked). */
+#define MSHA_DEVICE_ARENA_SLACK 64u
+/* Device-resident message starts must be multiples of this. */
+#define MSHA_DEVICE_ALIGN 16u
+
+typedef struct msha_ctx msha_ctx;
+
+typedef struct {
+  uint64_t calls;          /* batch calls completed */
+  uint64_t messages;       /* digests produced */
+  uint64_t message_bytes;  /* sum of unpadded message lengths */
+  uint64_t blocks;         /* 64-byte compressions performed */
+  double pack_ms;          /* host packing into pinned staging */
+  double h2d_ms;           /* host -> device copies (wall, last call) */
+  double kernel_ms;        /* kernel time (HIP events, last call, max over devices) */
+  double d2h_ms;           /* device -> host copies (wall, last call) */
+} msha_stats;
+
+uint32_t msha_abi_version(void);
+
+/* Number of visible HIP devices (0 when none). */
+int msha_device_count(int* n);
+
+/* Create a context on the devices in device_mask (bit i = HIP device i);
+ * device_mask == 0 means "device 0". Independent actions are sharded across
+ * the masked devices (one stream per device, partitioned by cumulative block
+ * count); no inter-GPU collective is used. */
+int msha_ctx_create(uint32_t device_mask, msha_ctx** out);
+void msha_ctx_destroy(msha_ctx* ctx);
+const char* msha_last_error(const msha_ctx* ctx);
+int msha_get_stats(const msha_ctx* ctx, msha_stats* out);
+
+/*
+ * ProcessHashActions over a packed arena (serial.go:180-198).
+ *   part j           = arena[part_off[j] : part_off[j] + part_len[j]]
+ *   action i's parts = parts [action_part_begin[i], action_part_begin[i+1])
+ *   out[32*i ...]    = SHA-256(concatenation of action i's parts)
+ * Zero-part actions hash the empty string; empty parts contribute nothing;
+ * parts may overlap or repeat. action_part_begin has n_actions+1 entries,
+ * non-decreasing, action_part_begin[0] == 0, last == n_parts.
+ */
+int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
+                      const uint64_t* part_off, const uint64_t* part_len, uint64_t n_parts,
+                      const uint64_t* action_part_begin, uint64_t n_actions, uint8_t* out);
+
+/*
+ * One-part messages (request digests, clients.go:189-192; or any action whose
+ * parts the caller already concatenated): out[32*i] = SHA-256(arena[off[i] :
+ * off[i]+len[i]]). Several messages may alias one payload (EpochChange
+ * re-hashing, epoch_target.go:486-505): it is copied to the device once.
+ */
+int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
+                      const uint64_t* off, const uint64_t* len, uint64_t n, uint8_t* out);
+
+/*
+ * Batch / VerifyBatch digest over request-ack digests (sequence.go:155-158,
+ * batch_tracker.go:175-178) when every part is a 32-byte digest:
+ *   out[32*i] = SHA-256(table[idx[k]] for k in [begin[i], begin[i+1]))
+ * table is n_table x 32 bytes; begin has n+1 entries.
+ */
+int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table,
+                           const uint32_t* idx, uint64_t n_idx, const uint64_t* begin,
+                           uint64_t n, uint8_t* out);
+
+/*
+ * Device-resident (kernel-resident) forms, for callers that keep inputs in
+ * HBM: every pointer is device memory on the context's FIRST device and the
+ * work is enqueued on `stream` (a hipStream_t, NULL = the context's own
+ * stream); the call returns after enqueueing. Arena rules: message starts
+ * MSHA_DEVICE_ALIGN-aligned, MSHA_DEVICE_ARENA_SLACK readable bytes after the
+ * last message. A misaligned start is reported by msha_device_status() and its
+ * digest is zeroed (never a wrong digest).
+ */
+int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                             const uint64_t* d_len, uint64_t n, uint8_t* d_out, void* stream);
+int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t stride,
+                               uint64_t msg_len, uint64_t n, uint8_t* d_out, void* stream);
+int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const uint32_t* d_idx,
+                                  const uint64_t* d_begin, uint64_t n, uint8_t* d_out,
+                                  void* stream);
+/* Synchronizes the context's first device and reports (then clears) any
+ * device-side error flag raised by *_device calls: MSHA_OK or MSHA_ERR_ALIGNMENT. */
+int msha_device_status(msha_ctx* ctx);
+
+/* Pinned host memory for callers that want zero-copy staging. */
+int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p);
+int msha_pinned_free(msha_ctx* ctx, void* p);
+
+/*
+ * Host-only helpers (no GPU needed).
+ * msha_blocks_for_len: number of 64-byte compressions for an L-byte message,
+ *   floor(L/64) + (L%64 < 56 ? 1 : 2)  (FIPS 180-4 5.1.1 padding).
+ * msha_partition_by_blocks: split messages [0, n) into n_shards contiguous
+ *   ranges of near-equal cumulative block count; bounds[0..n_shards]
+ *   (bounds[0] = 0, bounds[n_shards] = n). Used for multi-GPU sharding.
+ */
+uint64_t msha_blocks_for_len(uint64_t len);
+int msha_partition_by_blocks(const uint64_t* len, uint64_t n, uint32_t n_shards,
+                             uint64_t* bounds);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MIRSHA_H_ */

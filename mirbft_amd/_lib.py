@@ -1,0 +1,109 @@
+"""ctypes binding of libmirsha.so (the C ABI in include/mirsha.h).
+
+The library is built in-tree (``mirbft_amd/libmirsha.so``, see
+``mirbft_amd/csrc/Makefile`` and ``__graft_entry__.build()``). Loading fails
+loudly when it is missing: there is no Python or CPU fallback for hashing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmirsha.so")
+HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
+
+MSHA_OK = 0
+MSHA_ERR_INVALID_ARG = 1
+MSHA_ERR_NO_DEVICE = 2
+MSHA_ERR_HIP = 3
+MSHA_ERR_OUT_OF_MEMORY = 4
+MSHA_ERR_ALIGNMENT = 5
+MSHA_DEVICE_ARENA_SLACK = 64
+MSHA_DEVICE_ALIGN = 16
+
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_u64p = ctypes.POINTER(ctypes.c_uint64)
+_ctxp = ctypes.c_void_p
+
+
+class MshaStats(ctypes.Structure):
+    _fields_ = [
+        ("calls", ctypes.c_uint64),
+        ("messages", ctypes.c_uint64),
+        ("message_bytes", ctypes.c_uint64),
+        ("blocks", ctypes.c_uint64),
+        ("pack_ms", ctypes.c_double),
+        ("h2d_ms", ctypes.c_double),
+        ("kernel_ms", ctypes.c_double),
+        ("d2h_ms", ctypes.c_double),
+    ]
+
+
+# name -> (restype, argtypes)
+SIGNATURES = {
+    "msha_abi_version": (ctypes.c_uint32, []),
+    "msha_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    "msha_ctx_create": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_ctxp)]),
+    "msha_ctx_destroy": (None, [_ctxp]),
+    "msha_last_error": (ctypes.c_char_p, [_ctxp]),
+    "msha_get_stats": (ctypes.c_int, [_ctxp, ctypes.POINTER(MshaStats)]),
+    "msha_hash_actions": (ctypes.c_int, [_ctxp, _u8p, ctypes.c_uint64, _u64p, _u64p, ctypes.c_uint64,
+                                         _u64p, ctypes.c_uint64, _u8p]),
+    "msha_digest_batch": (ctypes.c_int, [_ctxp, _u8p, ctypes.c_uint64, _u64p, _u64p, ctypes.c_uint64,
+                                         _u8p]),
+    "msha_digest_of_digests": (ctypes.c_int, [_ctxp, _u8p, ctypes.c_uint64, _u32p, ctypes.c_uint64,
+                                              _u64p, ctypes.c_uint64, _u8p]),
+    "msha_digest_batch_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "msha_digest_uniform_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
+                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+    "msha_digest_of_digests_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_void_p,
+                                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                     ctypes.c_void_p]),
+    "msha_device_status": (ctypes.c_int, [_ctxp]),
+    "msha_pinned_alloc": (ctypes.c_int, [_ctxp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
+    "msha_pinned_free": (ctypes.c_int, [_ctxp, ctypes.c_void_p]),
+    "msha_blocks_for_len": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "msha_partition_by_blocks": (ctypes.c_int, [_u64p, ctypes.c_uint64, ctypes.c_uint32, _u64p]),
+}
+
+_lib = None
+
+
+def header_symbols() -> list[str]:
+    """Every function the public header declares."""
+    with open(HEADER_PATH) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[\w\s\*]+?\b(msha_\w+)\s*\(", text, re.M)))
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmirsha.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "or `make -C mirbft_amd/csrc` (there is no CPU fallback)")
+    # One HIP runtime per process: torch ships its own libamdhip64 (NEEDED as
+    # "libamdhip64.so", SONAME libamdhip64.so.7). Loaded first, it satisfies our
+    # NEEDED libamdhip64.so.7 by SONAME and both share it; loaded second, torch
+    # would bring a second runtime and fail to initialise. So when torch is
+    # installed it is imported before libmirsha.so is opened.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(L, name)
+        fn.restype = res
+        fn.argtypes = args
+    if L.msha_abi_version() != 1:
+        raise ImportError("libmirsha ABI version mismatch")
+    _lib = L
+    return L

@@ -1,0 +1,205 @@
+// HIP kernels for the batched SHA-256 digest engine (gfx950 only).
+//
+// Replaces, per message, Go crypto/sha256 as driven by
+// processor.ProcessHashActions (/root/reference/pkg/processor/serial.go:180-198):
+// every lane of a wavefront owns one hash action's message and runs
+// New/Write/Sum for it entirely in VGPRs. The kernels apply FIPS 180-4 padding
+// themselves from the length, so the host never writes padding bytes.
+//
+// Data layout in HBM (see DESIGN.md "Data layout"):
+//   arena  : message bytes, each message 16-byte aligned (the host packer
+//            guarantees this; other alignments take a slower correct path)
+//   off/len: uint64 per message (several messages may alias one payload)
+//   order  : optional uint32 permutation (size-class binning: lanes of a wave
+//            get messages of equal block count so no lane idles)
+//   out    : 32 bytes per message, digest i at out + 32*i
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sha256_device.hpp"
+#include "kernels.hpp"
+
+namespace msha {
+
+__device__ __forceinline__ void load_block16(const uint8_t* p, uint32_t (&raw)[16]) {
+  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u32x4 v = q[i];
+    raw[4 * i + 0] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
+  }
+}
+
+__device__ __forceinline__ void to_words(const uint32_t (&raw)[16], uint32_t (&w)[16]) {
+#pragma unroll
+  for (int j = 0; j < 16; ++j) w[j] = bswap(raw[j]);
+}
+
+// Hash one message of `len` bytes starting at p (device memory, 16-byte
+// aligned, with kArenaSlack (kernels.hpp) readable bytes after the arena's last
+// message) into out. One compress() call site: full blocks, the tail block
+// and the optional extra length block all go through the same loop body.
+// The tail block is read as a whole 64-byte block (it may run into the next
+// message or the slack); build_tail() masks every byte at or past `len`.
+// PREFETCH=true loads block b+1 while block b is compressed (16 more VGPRs):
+// used when there are too few waves per SIMD to hide HBM latency by
+// occupancy (few, long messages).
+template <bool PREFETCH>
+__device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uint8_t* out) {
+  State s;
+  state_init(s);
+  const uint32_t nfull = (uint32_t)(len >> 6);  // < 2^32 blocks: messages < 256 GiB
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint32_t nblocks = nfull + (r < 56 ? 1 : 2);
+  uint32_t raw[16];
+  uint32_t w[16];
+  if (PREFETCH) load_block16(p, raw);
+  for (uint32_t b = 0; b < nblocks; ++b) {
+    if (!PREFETCH && b <= nfull) load_block16(p + 64 * (uint64_t)b, raw);
+    if (b < nfull) {
+      to_words(raw, w);
+      if (PREFETCH) load_block16(p + 64 * (uint64_t)(b + 1), raw);
+    } else if (b == nfull) {
+      // Launder r so the 16 per-dword tail masks are built here, once, and
+      // not hoisted out of the loop into 32 loop-long VGPRs.
+      uint32_t rr = r;
+      asm volatile("" : "+v"(rr));
+      build_tail(raw, rr, len, w);
+    } else {
+      length_block(len, w);
+    }
+    compress(s, w);
+  }
+  store_digest(s, out);
+}
+
+// Misaligned message start: not produced by the library's packers; flagged
+// (device word *err |= 1) and the digest zeroed rather than computed wrongly.
+__device__ __forceinline__ bool check_aligned(const uint8_t* p, uint8_t* out, uint32_t* err) {
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) return true;
+  atomicOr(err, 1u);
+  reinterpret_cast<uint4*>(out)[0] = make_uint4(0, 0, 0, 0);
+  reinterpret_cast<uint4*>(out)[1] = make_uint4(0, 0, 0, 0);
+  return false;
+}
+
+template <bool PREFETCH>
+__global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restrict__ arena,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint64_t* __restrict__ len,
+                                                      const uint32_t* __restrict__ order,
+                                                      uint64_t n, uint8_t* __restrict__ out,
+                                                      uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t m = order ? (uint64_t)order[i] : i;
+  const uint8_t* p = arena + off[m];
+  if (check_aligned(p, out + 32 * m, err)) hash_message<PREFETCH>(p, len[m], out + 32 * m);
+}
+
+// Uniform layout: message i is arena[i*stride : i*stride + msg_len].
+template <bool PREFETCH>
+__global__ __launch_bounds__(256, 8) void k_digest_uniform(const uint8_t* __restrict__ arena,
+                                                        uint64_t stride, uint64_t msg_len,
+                                                        uint64_t n, uint8_t* __restrict__ out,
+                                                        uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* p = arena + i * stride;
+  if (check_aligned(p, out + 32 * i, err)) hash_message<PREFETCH>(p, msg_len, out + 32 * i);
+}
+
+// Digest-of-digests (Batch / VerifyBatch actions, /root/reference/pkg/statemachine/
+// sequence.go:155-158, batch_tracker.go:175-178): out[i] = SHA256(concat over
+// k in [begin[i], begin[i+1]) of table[idx[k]]), every part a 32-byte digest
+// already resident in HBM (e.g. request digests produced by k_digest_batch).
+// Two digests fill one 64-byte block; the tail block holds 0 or 1 digest.
+__global__ __launch_bounds__(256, 8) void k_digest_of_digests(const uint8_t* __restrict__ table,
+                                                           const uint32_t* __restrict__ idx,
+                                                           const uint64_t* __restrict__ begin,
+                                                           uint64_t n, uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t k0 = begin[i], cnt = begin[i + 1] - k0;
+  const uint64_t len = 32 * cnt;
+  const uint4* tab = reinterpret_cast<const uint4*>(table);
+  State s;
+  state_init(s);
+  uint32_t w[16];
+  uint64_t k = 0;
+  for (; k + 2 <= cnt; k += 2) {
+    const uint4* d0 = tab + 2 * (uint64_t)idx[k0 + k];
+    const uint4* d1 = tab + 2 * (uint64_t)idx[k0 + k + 1];
+    uint4 v0 = d0[0], v1 = d0[1], v2 = d1[0], v3 = d1[1];
+    w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
+    w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
+    w[8] = bswap(v2.x); w[9] = bswap(v2.y); w[10] = bswap(v2.z); w[11] = bswap(v2.w);
+    w[12] = bswap(v3.x); w[13] = bswap(v3.y); w[14] = bswap(v3.z); w[15] = bswap(v3.w);
+    compress(s, w);
+  }
+  const uint64_t bits = len * 8;
+  if (k < cnt) {  // one digest left: 32 bytes + 0x80 + zeros + length fit one block
+    const uint4* d0 = tab + 2 * (uint64_t)idx[k0 + k];
+    uint4 v0 = d0[0], v1 = d0[1];
+    w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
+    w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
+    w[8] = 0x80000000u;
+#pragma unroll
+    for (int j = 9; j < 14; ++j) w[j] = 0;
+  } else {
+    w[0] = 0x80000000u;
+#pragma unroll
+    for (int j = 1; j < 14; ++j) w[j] = 0;
+  }
+  w[14] = (uint32_t)(bits >> 32);
+  w[15] = (uint32_t)bits;
+  compress(s, w);
+  store_digest(s, out + 32 * i);
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (host side). Grids are one lane per message, 256-thread blocks.
+// ---------------------------------------------------------------------------
+static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
+
+// Fewer than ~3 waves per SIMD cannot hide HBM latency by occupancy: use the
+// register-prefetching variant then.
+static inline bool want_prefetch(uint64_t n, int cus) { return n < (uint64_t)cus * 4 * 64 * 3; }
+
+hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
+                               const uint32_t* order, uint64_t n, uint8_t* out, uint32_t* err,
+                               int cus, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (want_prefetch(n, cus))
+    hipLaunchKernelGGL(k_digest_batch<true>, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
+                       order, n, out, err);
+  else
+    hipLaunchKernelGGL(k_digest_batch<false>, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
+                       order, n, out, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
+                                 uint64_t n, uint8_t* out, uint32_t* err, int cus,
+                                 hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  if (want_prefetch(n, cus))
+    hipLaunchKernelGGL(k_digest_uniform<true>, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
+                       msg_len, n, out, err);
+  else
+    hipLaunchKernelGGL(k_digest_uniform<false>, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
+                       msg_len, n, out, err);
+  return hipGetLastError();
+}
+
+hipError_t launch_digest_of_digests(const uint8_t* table, const uint32_t* idx,
+                                    const uint64_t* begin, uint64_t n, uint8_t* out,
+                                    hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_digest_of_digests, dim3(grid_for(n)), dim3(256), 0, st, table, idx, begin,
+                     n, out);
+  return hipGetLastError();
+}
+
+}  // namespace msha

@@ -1,0 +1,22 @@
+// Host-side launchers for the gfx950 SHA-256 kernels (kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace msha {
+
+// Bytes that must be readable after the last message of a device arena: the
+// kernels read a message's final block as one whole 64-byte block.
+constexpr uint64_t kArenaSlack = 64;
+
+hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
+                               const uint32_t* order, uint64_t n, uint8_t* out, uint32_t* err,
+                               int cus, hipStream_t st);
+hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
+                                 uint64_t n, uint8_t* out, uint32_t* err, int cus,
+                                 hipStream_t st);
+hipError_t launch_digest_of_digests(const uint8_t* table, const uint32_t* idx,
+                                    const uint64_t* begin, uint64_t n, uint8_t* out,
+                                    hipStream_t st);
+
+}  // namespace msha

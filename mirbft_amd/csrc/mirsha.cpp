@@ -1,0 +1,622 @@
+// libmirsha: host side of the MI355X batched SHA-256 engine (C ABI in include/mirsha.h).
+//
+// One call == one processor.ProcessHashActions over a whole ActionList
+// (/root/reference/pkg/processor/serial.go:180-198): validate, pack into
+// pinned staging, shard across the context's GPUs by cumulative block count,
+// H2D per shard on that GPU's stream, one kernel launch per shard, D2H of the
+// digests, join. There is no collective and no CPU hashing anywhere here.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <exception>
+#include <new>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/mirsha.h"
+#include "kernels.hpp"
+
+namespace {
+
+struct MshaError : std::runtime_error {
+  int code;
+  MshaError(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHK(expr)                                                                         \
+  do {                                                                                       \
+    hipError_t e_ = (expr);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      throw MshaError(e_ == hipErrorOutOfMemory ? MSHA_ERR_OUT_OF_MEMORY : MSHA_ERR_HIP,     \
+                      std::string(#expr) + ": " + hipGetErrorString(e_));                    \
+  } while (0)
+
+thread_local std::string g_create_error;
+
+double now_ms() {
+  using namespace std::chrono;
+  return duration<double, std::milli>(steady_clock::now().time_since_epoch()).count();
+}
+
+inline uint64_t blocks_for(uint64_t len) { return (len >> 6) + ((len & 63) < 56 ? 1 : 2); }
+inline uint64_t round16(uint64_t x) { return (x + 15) & ~uint64_t(15); }
+
+// Growable device buffer (never shrinks; reallocation only between calls).
+struct DevBuf {
+  void* p = nullptr;
+  uint64_t cap = 0;
+  void ensure(uint64_t bytes) {
+    if (bytes <= cap) return;
+    if (p) HIPCHK(hipFree(p));
+    p = nullptr;
+    cap = 0;
+    uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
+    HIPCHK(hipMalloc(&p, want));
+    cap = want;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Growable pinned host buffer.
+struct PinBuf {
+  void* p = nullptr;
+  uint64_t cap = 0;
+  void ensure(uint64_t bytes) {
+    if (bytes <= cap) return;
+    if (p) HIPCHK(hipHostFree(p));
+    p = nullptr;
+    cap = 0;
+    uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
+    HIPCHK(hipHostMalloc(&p, want, hipHostMallocPortable));
+    cap = want;
+  }
+  void release() {
+    if (p) (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T> T* as() const { return static_cast<T*>(p); }
+};
+
+// Per-GPU state: stream, timing events, device buffers, pinned staging.
+struct Device {
+  int id = 0;
+  int cus = 256;
+  hipStream_t stream = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  DevBuf arena, off, len, order, out, err, idx, begin, table;
+  PinBuf h_arena, h_meta, h_out;
+  // per-call shard description
+  uint64_t lo = 0, hi = 0;        // message/action range
+  uint64_t arena_bytes = 0;       // staged arena size (without slack)
+  bool use_order = false;
+  void release() {
+    for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table}) b->release();
+    for (PinBuf* b : {&h_arena, &h_meta, &h_out}) b->release();
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (stream) (void)hipStreamDestroy(stream);
+    ev0 = ev1 = nullptr;
+    stream = nullptr;
+  }
+};
+
+// Descending-block-count permutation (LSD radix on 32-bit keys) so every
+// wavefront gets messages of equal length and no lane idles.
+void order_by_blocks_desc(const uint64_t* len, uint64_t n, uint32_t* order, std::vector<uint32_t>& tmp) {
+  std::vector<uint32_t> key(n);
+  for (uint64_t i = 0; i < n; ++i) {
+    uint64_t b = blocks_for(len[i]);
+    key[i] = 0xffffffffu - (uint32_t)std::min<uint64_t>(b, 0xffffffffu);
+  }
+  tmp.resize(n);
+  uint32_t* src = order;
+  uint32_t* dst = tmp.data();
+  for (uint64_t i = 0; i < n; ++i) src[i] = (uint32_t)i;
+  for (int shift = 0; shift < 32; shift += 16) {
+    std::vector<uint64_t> cnt(65537, 0);
+    for (uint64_t i = 0; i < n; ++i) cnt[((key[src[i]] >> shift) & 0xffff) + 1]++;
+    for (int d = 0; d < 65536; ++d) cnt[d + 1] += cnt[d];
+    for (uint64_t i = 0; i < n; ++i) dst[cnt[(key[src[i]] >> shift) & 0xffff]++] = src[i];
+    std::swap(src, dst);
+  }
+  // two passes: result is back in `order`
+}
+
+bool all_equal_blocks(const uint64_t* len, uint64_t n) {
+  if (n == 0) return true;
+  uint64_t b0 = blocks_for(len[0]);
+  for (uint64_t i = 1; i < n; ++i)
+    if (blocks_for(len[i]) != b0) return false;
+  return true;
+}
+
+void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
+  uint64_t total = 0;
+  for (uint64_t i = 0; i < n; ++i) total += blocks_for(len[i]);
+  bounds[0] = 0;
+  uint64_t acc = 0, i = 0;
+  for (uint32_t s = 1; s < k; ++s) {
+    // first index whose cumulative block count reaches s/k of the total
+    const long double target = (long double)total * s / k;
+    while (i < n && (long double)acc + blocks_for(len[i]) / 2.0L < target) acc += blocks_for(len[i++]);
+    bounds[s] = i;
+  }
+  bounds[k] = n;
+}
+
+}  // namespace
+
+struct msha_ctx {
+  std::vector<Device> devs;
+  std::string err;
+  msha_stats stats{};
+  std::vector<void*> pinned;  // allocations handed out by msha_pinned_alloc
+  std::vector<uint32_t> sort_tmp;
+  std::vector<uint64_t> tmp_len;
+};
+
+namespace {
+
+int fail(msha_ctx* ctx, int code, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  return code;
+}
+
+template <class F>
+int guarded(msha_ctx* ctx, F&& f) {
+  try {
+    f();
+    if (ctx) ctx->err.clear();
+    return MSHA_OK;
+  } catch (const MshaError& e) {
+    return fail(ctx, e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return fail(ctx, MSHA_ERR_OUT_OF_MEMORY, "host allocation failed");
+  } catch (const std::exception& e) {
+    return fail(ctx, MSHA_ERR_HIP, e.what());
+  } catch (...) {
+    return fail(ctx, MSHA_ERR_HIP, "unknown error");
+  }
+}
+
+// Shared tail of the host-memory entry points: `pack(dev)` fills dev.h_arena
+// and dev.h_meta (off then len, uint64 each, shard-local) for messages
+// [dev.lo, dev.hi); this function ships them, launches and collects.
+template <class Pack>
+void run_sharded(msha_ctx* ctx, uint64_t n, const uint64_t* msg_len_for_partition,
+                 uint8_t* out, Pack&& pack) {
+  const uint32_t k = (uint32_t)ctx->devs.size();
+  std::vector<uint64_t> bounds(k + 1);
+  if (k == 1) {
+    bounds[0] = 0;
+    bounds[1] = n;
+  } else {
+    partition(msg_len_for_partition, n, k, bounds.data());
+  }
+  double t0 = now_ms();
+  for (uint32_t s = 0; s < k; ++s) {
+    Device& d = ctx->devs[s];
+    d.lo = bounds[s];
+    d.hi = bounds[s + 1];
+    pack(d);
+  }
+  double t1 = now_ms();
+  // Enqueue H2D + kernel + D2H on every device, then join.
+  for (uint32_t s = 0; s < k; ++s) {
+    Device& d = ctx->devs[s];
+    const uint64_t m = d.hi - d.lo;
+    if (m == 0) continue;
+    HIPCHK(hipSetDevice(d.id));
+    d.arena.ensure(d.arena_bytes + msha::kArenaSlack);
+    d.off.ensure(8 * m);
+    d.len.ensure(8 * m);
+    d.out.ensure(32 * m);
+    d.err.ensure(4);
+    const uint64_t* h_off = d.h_meta.as<uint64_t>();
+    const uint64_t* h_len = h_off + m;
+    if (d.arena_bytes)
+      HIPCHK(hipMemcpyAsync(d.arena.p, d.h_arena.p, d.arena_bytes, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(hipMemcpyAsync(d.off.p, h_off, 8 * m, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(hipMemcpyAsync(d.len.p, h_len, 8 * m, hipMemcpyHostToDevice, d.stream));
+    const uint32_t* dorder = nullptr;
+    if (d.use_order) {
+      d.order.ensure(4 * m);
+      HIPCHK(hipMemcpyAsync(d.order.p, h_len + m, 4 * m, hipMemcpyHostToDevice, d.stream));
+      dorder = d.order.as<uint32_t>();
+    }
+    HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
+    HIPCHK(hipEventRecord(d.ev0, d.stream));
+    HIPCHK(msha::launch_digest_batch(d.arena.as<uint8_t>(), d.off.as<uint64_t>(),
+                                     d.len.as<uint64_t>(), dorder, m, d.out.as<uint8_t>(),
+                                     d.err.as<uint32_t>(), d.cus, d.stream));
+    HIPCHK(hipEventRecord(d.ev1, d.stream));
+    d.h_out.ensure(32 * m + 4);
+    HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost,
+                          d.stream));
+  }
+  double kernel_ms = 0;
+  for (uint32_t s = 0; s < k; ++s) {
+    Device& d = ctx->devs[s];
+    const uint64_t m = d.hi - d.lo;
+    if (m == 0) continue;
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
+    kernel_ms = std::max<double>(kernel_ms, ms);
+    uint32_t errflag;
+    std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+    if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
+    std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
+  }
+  double t2 = now_ms();
+  ctx->stats.calls++;
+  ctx->stats.pack_ms = t1 - t0;
+  ctx->stats.h2d_ms = t2 - t1;  // wall of enqueue..join (H2D + kernel + D2H)
+  ctx->stats.kernel_ms = kernel_ms;
+  ctx->stats.d2h_ms = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+uint32_t msha_abi_version(void) { return MSHA_ABI_VERSION; }
+
+int msha_device_count(int* n) {
+  if (!n) return MSHA_ERR_INVALID_ARG;
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) {
+    (void)hipGetLastError();
+    c = 0;
+  }
+  *n = c;
+  return MSHA_OK;
+}
+
+int msha_ctx_create(uint32_t device_mask, msha_ctx** out) {
+  if (!out) return MSHA_ERR_INVALID_ARG;
+  *out = nullptr;
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
+    (void)hipGetLastError();
+    g_create_error = "no HIP device available (the engine has no CPU fallback)";
+    return MSHA_ERR_NO_DEVICE;
+  }
+  if (device_mask == 0) device_mask = 1;
+  msha_ctx* ctx = new (std::nothrow) msha_ctx();
+  if (!ctx) return MSHA_ERR_OUT_OF_MEMORY;
+  int rc = guarded(ctx, [&] {
+    for (int i = 0; i < 32; ++i) {
+      if (!(device_mask & (1u << i))) continue;
+      if (i >= count) throw MshaError(MSHA_ERR_NO_DEVICE, "device_mask names device " + std::to_string(i) + " but only " + std::to_string(count) + " visible");
+      Device d;
+      d.id = i;
+      HIPCHK(hipSetDevice(i));
+      hipDeviceProp_t prop;
+      HIPCHK(hipGetDeviceProperties(&prop, i));
+      d.cus = prop.multiProcessorCount;
+      HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+      HIPCHK(hipEventCreate(&d.ev0));
+      HIPCHK(hipEventCreate(&d.ev1));
+      ctx->devs.push_back(d);
+    }
+  });
+  if (rc != MSHA_OK) {
+    g_create_error = ctx->err;
+    for (auto& d : ctx->devs) d.release();
+    delete ctx;
+    return rc;
+  }
+  *out = ctx;
+  return MSHA_OK;
+}
+
+void msha_ctx_destroy(msha_ctx* ctx) {
+  if (!ctx) return;
+  for (auto& d : ctx->devs) {
+    (void)hipSetDevice(d.id);
+    (void)hipStreamSynchronize(d.stream);
+    d.release();
+  }
+  for (void* p : ctx->pinned) (void)hipHostFree(p);
+  delete ctx;
+}
+
+const char* msha_last_error(const msha_ctx* ctx) {
+  return ctx ? ctx->err.c_str() : g_create_error.c_str();
+}
+
+int msha_get_stats(const msha_ctx* ctx, msha_stats* out) {
+  if (!ctx || !out) return MSHA_ERR_INVALID_ARG;
+  *out = ctx->stats;
+  return MSHA_OK;
+}
+
+uint64_t msha_blocks_for_len(uint64_t len) { return blocks_for(len); }
+
+int msha_partition_by_blocks(const uint64_t* len, uint64_t n, uint32_t n_shards, uint64_t* bounds) {
+  if (!bounds || n_shards == 0 || (n && !len)) return MSHA_ERR_INVALID_ARG;
+  partition(len, n, n_shards, bounds);
+  return MSHA_OK;
+}
+
+int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, const uint64_t* off,
+                      const uint64_t* len, uint64_t n, uint8_t* out) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (n == 0) return MSHA_OK;
+  if (!off || !len || !out || (arena_len && !arena))
+    return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
+  for (uint64_t i = 0; i < n; ++i)
+    if (len[i] > arena_len || off[i] > arena_len - len[i])
+      return fail(ctx, MSHA_ERR_INVALID_ARG,
+                  "message " + std::to_string(i) + " [off+len] outside arena");
+  return guarded(ctx, [&] {
+    bool aligned = true;
+    for (uint64_t i = 0; i < n && aligned; ++i) aligned = (off[i] & 15) == 0;
+    run_sharded(ctx, n, len, out, [&](Device& d) {
+      const uint64_t m = d.hi - d.lo;
+      if (m == 0) { d.arena_bytes = 0; return; }
+      const bool ord = !all_equal_blocks(len + d.lo, m);
+      d.use_order = ord;
+      d.h_meta.ensure(16 * m + (ord ? 4 * m : 0));
+      uint64_t* h_off = d.h_meta.as<uint64_t>();
+      uint64_t* h_len = h_off + m;
+      if (aligned) {
+        // Payloads are already 16-byte aligned: ship the span the shard
+        // references once (aliased payloads are copied once per GPU).
+        uint64_t lo = UINT64_MAX, hi = 0;
+        for (uint64_t i = d.lo; i < d.hi; ++i) {
+          lo = std::min(lo, off[i]);
+          hi = std::max(hi, off[i] + len[i]);
+        }
+        lo &= ~uint64_t(15);
+        d.arena_bytes = round16(hi - lo);
+        d.h_arena.ensure(d.arena_bytes);
+        std::memcpy(d.h_arena.p, arena + lo, hi - lo);
+        for (uint64_t i = 0; i < m; ++i) {
+          h_off[i] = off[d.lo + i] - lo;
+          h_len[i] = len[d.lo + i];
+        }
+      } else {
+        uint64_t total = 0;
+        for (uint64_t i = d.lo; i < d.hi; ++i) total += round16(len[i]);
+        d.arena_bytes = total;
+        d.h_arena.ensure(total);
+        uint64_t pos = 0;
+        for (uint64_t i = 0; i < m; ++i) {
+          std::memcpy(d.h_arena.as<uint8_t>() + pos, arena + off[d.lo + i], len[d.lo + i]);
+          h_off[i] = pos;
+          h_len[i] = len[d.lo + i];
+          pos += round16(len[d.lo + i]);
+        }
+      }
+      if (ord) order_by_blocks_desc(h_len, m, reinterpret_cast<uint32_t*>(h_len + m), ctx->sort_tmp);
+    });
+    uint64_t bytes = 0, blocks = 0;
+    for (uint64_t i = 0; i < n; ++i) { bytes += len[i]; blocks += blocks_for(len[i]); }
+    ctx->stats.messages += n;
+    ctx->stats.message_bytes += bytes;
+    ctx->stats.blocks += blocks;
+  });
+}
+
+int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
+                      const uint64_t* part_off, const uint64_t* part_len, uint64_t n_parts,
+                      const uint64_t* action_part_begin, uint64_t n_actions, uint8_t* out) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (n_actions == 0) return MSHA_OK;
+  if (!action_part_begin || !out || (n_parts && (!part_off || !part_len)) || (arena_len && !arena))
+    return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
+  if (action_part_begin[0] != 0 || action_part_begin[n_actions] != n_parts)
+    return fail(ctx, MSHA_ERR_INVALID_ARG, "action_part_begin must start at 0 and end at n_parts");
+  for (uint64_t i = 0; i < n_actions; ++i)
+    if (action_part_begin[i + 1] < action_part_begin[i])
+      return fail(ctx, MSHA_ERR_INVALID_ARG, "action_part_begin must be non-decreasing");
+  for (uint64_t j = 0; j < n_parts; ++j)
+    if (part_len[j] > arena_len || part_off[j] > arena_len - part_len[j])
+      return fail(ctx, MSHA_ERR_INVALID_ARG, "part " + std::to_string(j) + " outside arena");
+  return guarded(ctx, [&] {
+    // Message length of each action = sum of its parts (h.Write appends).
+    std::vector<uint64_t>& alen = ctx->tmp_len;
+    alen.assign(n_actions, 0);
+    for (uint64_t i = 0; i < n_actions; ++i)
+      for (uint64_t j = action_part_begin[i]; j < action_part_begin[i + 1]; ++j) alen[i] += part_len[j];
+    run_sharded(ctx, n_actions, alen.data(), out, [&](Device& d) {
+      const uint64_t m = d.hi - d.lo;
+      if (m == 0) { d.arena_bytes = 0; return; }
+      const bool ord = !all_equal_blocks(alen.data() + d.lo, m);
+      d.use_order = ord;
+      d.h_meta.ensure(16 * m + (ord ? 4 * m : 0));
+      uint64_t* h_off = d.h_meta.as<uint64_t>();
+      uint64_t* h_len = h_off + m;
+      uint64_t total = 0;
+      for (uint64_t i = d.lo; i < d.hi; ++i) total += round16(alen[i]);
+      d.arena_bytes = total;
+      d.h_arena.ensure(total);
+      uint8_t* dst = d.h_arena.as<uint8_t>();
+      uint64_t pos = 0;
+      for (uint64_t i = 0; i < m; ++i) {
+        const uint64_t a = d.lo + i;
+        h_off[i] = pos;
+        h_len[i] = alen[a];
+        uint64_t q = pos;
+        for (uint64_t j = action_part_begin[a]; j < action_part_begin[a + 1]; ++j) {
+          std::memcpy(dst + q, arena + part_off[j], part_len[j]);
+          q += part_len[j];
+        }
+        pos += round16(alen[a]);
+      }
+      if (ord) order_by_blocks_desc(h_len, m, reinterpret_cast<uint32_t*>(h_len + m), ctx->sort_tmp);
+    });
+    uint64_t bytes = 0, blocks = 0;
+    for (uint64_t i = 0; i < n_actions; ++i) { bytes += alen[i]; blocks += blocks_for(alen[i]); }
+    ctx->stats.messages += n_actions;
+    ctx->stats.message_bytes += bytes;
+    ctx->stats.blocks += blocks;
+  });
+}
+
+int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table,
+                           const uint32_t* idx, uint64_t n_idx, const uint64_t* begin, uint64_t n,
+                           uint8_t* out) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (n == 0) return MSHA_OK;
+  if (!begin || !out || (n_idx && !idx) || (n_table && !table))
+    return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
+  if (begin[0] != 0 || begin[n] != n_idx)
+    return fail(ctx, MSHA_ERR_INVALID_ARG, "begin must start at 0 and end at n_idx");
+  for (uint64_t i = 0; i < n; ++i)
+    if (begin[i + 1] < begin[i]) return fail(ctx, MSHA_ERR_INVALID_ARG, "begin must be non-decreasing");
+  for (uint64_t k = 0; k < n_idx; ++k)
+    if (idx[k] >= n_table) return fail(ctx, MSHA_ERR_INVALID_ARG, "idx out of table range");
+  return guarded(ctx, [&] {
+    std::vector<uint64_t>& alen = ctx->tmp_len;
+    alen.resize(n);
+    for (uint64_t i = 0; i < n; ++i) alen[i] = 32 * (begin[i + 1] - begin[i]);
+    const uint32_t k = (uint32_t)ctx->devs.size();
+    std::vector<uint64_t> bounds(k + 1);
+    partition(alen.data(), n, k, bounds.data());
+    double t0 = now_ms();
+    for (uint32_t s = 0; s < k; ++s) {
+      Device& d = ctx->devs[s];
+      const uint64_t lo = bounds[s], hi = bounds[s + 1], m = hi - lo;
+      d.lo = lo;
+      d.hi = hi;
+      if (m == 0) continue;
+      const uint64_t i0 = begin[lo], i1 = begin[hi];
+      HIPCHK(hipSetDevice(d.id));
+      d.table.ensure(32 * std::max<uint64_t>(n_table, 1));
+      d.idx.ensure(4 * std::max<uint64_t>(i1 - i0, 1));
+      d.begin.ensure(8 * (m + 1));
+      d.out.ensure(32 * m);
+      d.h_meta.ensure(8 * (m + 1));
+      uint64_t* hb = d.h_meta.as<uint64_t>();
+      for (uint64_t i = 0; i <= m; ++i) hb[i] = begin[lo + i] - i0;
+      if (n_table) HIPCHK(hipMemcpyAsync(d.table.p, table, 32 * n_table, hipMemcpyHostToDevice, d.stream));
+      if (i1 > i0) HIPCHK(hipMemcpyAsync(d.idx.p, idx + i0, 4 * (i1 - i0), hipMemcpyHostToDevice, d.stream));
+      HIPCHK(hipMemcpyAsync(d.begin.p, hb, 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
+      HIPCHK(hipEventRecord(d.ev0, d.stream));
+      HIPCHK(msha::launch_digest_of_digests(d.table.as<uint8_t>(), d.idx.as<uint32_t>(),
+                                            d.begin.as<uint64_t>(), m, d.out.as<uint8_t>(), d.stream));
+      HIPCHK(hipEventRecord(d.ev1, d.stream));
+      d.h_out.ensure(32 * m);
+      HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+    }
+    double kernel_ms = 0;
+    for (uint32_t s = 0; s < k; ++s) {
+      Device& d = ctx->devs[s];
+      const uint64_t m = d.hi - d.lo;
+      if (m == 0) continue;
+      HIPCHK(hipSetDevice(d.id));
+      HIPCHK(hipStreamSynchronize(d.stream));
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
+      kernel_ms = std::max<double>(kernel_ms, ms);
+      std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
+    }
+    uint64_t blocks = 0;
+    for (uint64_t i = 0; i < n; ++i) blocks += blocks_for(alen[i]);
+    ctx->stats.calls++;
+    ctx->stats.messages += n;
+    ctx->stats.message_bytes += 32 * n_idx;
+    ctx->stats.blocks += blocks;
+    ctx->stats.kernel_ms = kernel_ms;
+    ctx->stats.h2d_ms = now_ms() - t0;
+  });
+}
+
+static int device_prologue(msha_ctx* ctx, void* stream, hipStream_t* st) {
+  if (!ctx || ctx->devs.empty()) return MSHA_ERR_INVALID_ARG;
+  Device& d = ctx->devs[0];
+  HIPCHK(hipSetDevice(d.id));
+  d.err.ensure(4);
+  *st = stream ? static_cast<hipStream_t>(stream) : d.stream;
+  return MSHA_OK;
+}
+
+int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                             const uint64_t* d_len, uint64_t n, uint8_t* d_out, void* stream) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (n == 0) return MSHA_OK;
+  if (!d_arena || !d_off || !d_len || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
+  return guarded(ctx, [&] {
+    hipStream_t st;
+    device_prologue(ctx, stream, &st);
+    Device& d = ctx->devs[0];
+    HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, nullptr, n, d_out, d.err.as<uint32_t>(),
+                                     d.cus, st));
+  });
+}
+
+int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t stride,
+                               uint64_t msg_len, uint64_t n, uint8_t* d_out, void* stream) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (n == 0) return MSHA_OK;
+  if (!d_arena || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
+  if (stride < msg_len) return fail(ctx, MSHA_ERR_INVALID_ARG, "stride < msg_len");
+  if (stride % MSHA_DEVICE_ALIGN) return fail(ctx, MSHA_ERR_ALIGNMENT, "stride must be a multiple of 16");
+  return guarded(ctx, [&] {
+    hipStream_t st;
+    device_prologue(ctx, stream, &st);
+    Device& d = ctx->devs[0];
+    HIPCHK(msha::launch_digest_uniform(d_arena, stride, msg_len, n, d_out, d.err.as<uint32_t>(), d.cus, st));
+  });
+}
+
+int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const uint32_t* d_idx,
+                                  const uint64_t* d_begin, uint64_t n, uint8_t* d_out, void* stream) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (n == 0) return MSHA_OK;
+  if (!d_table || !d_idx || !d_begin || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
+  return guarded(ctx, [&] {
+    hipStream_t st;
+    device_prologue(ctx, stream, &st);
+    HIPCHK(msha::launch_digest_of_digests(d_table, d_idx, d_begin, n, d_out, st));
+  });
+}
+
+int msha_device_status(msha_ctx* ctx) {
+  if (!ctx || ctx->devs.empty()) return MSHA_ERR_INVALID_ARG;
+  uint32_t flag = 0;
+  int rc = guarded(ctx, [&] {
+    Device& d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(hipDeviceSynchronize());
+    if (!d.err.p) return;
+    HIPCHK(hipMemcpy(&flag, d.err.p, 4, hipMemcpyDeviceToHost));
+    HIPCHK(hipMemset(d.err.p, 0, 4));
+  });
+  if (rc != MSHA_OK) return rc;
+  if (flag) return fail(ctx, MSHA_ERR_ALIGNMENT, "device arena message start not 16-byte aligned");
+  return MSHA_OK;
+}
+
+int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p) {
+  if (!ctx || !p) return MSHA_ERR_INVALID_ARG;
+  return guarded(ctx, [&] {
+    HIPCHK(hipSetDevice(ctx->devs[0].id));
+    HIPCHK(hipHostMalloc(p, std::max<uint64_t>(bytes, 1), hipHostMallocPortable));
+    ctx->pinned.push_back(*p);
+  });
+}
+
+int msha_pinned_free(msha_ctx* ctx, void* p) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  auto it = std::find(ctx->pinned.begin(), ctx->pinned.end(), p);
+  if (it == ctx->pinned.end()) return fail(ctx, MSHA_ERR_INVALID_ARG, "pointer not from msha_pinned_alloc");
+  ctx->pinned.erase(it);
+  return guarded(ctx, [&] { HIPCHK(hipHostFree(p)); });
+}
+
+}  // extern "C"

@@ -1,0 +1,184 @@
+"""Python handle on a libmirsha context (one or more GPUs).
+
+``Engine`` is a thin, allocation-light wrapper over the C ABI
+(include/mirsha.h). Host-memory calls take numpy arrays; device-resident calls
+take torch tensors already on the GPU (``torch`` supplies device memory and
+streams only -- all hashing happens in the HIP kernels of libmirsha.so).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import _lib as L
+
+
+class MshaError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libmirsha error {code}: {msg}")
+        self.code = code
+
+
+def _p(a: np.ndarray, t):
+    return a.ctypes.data_as(ctypes.POINTER(t))
+
+
+def blocks_for_len(length: int) -> int:
+    """FIPS 180-4 padded block count of an L-byte message (host-only helper)."""
+    return int(L.lib().msha_blocks_for_len(int(length)))
+
+
+def partition_by_blocks(lengths: np.ndarray, n_shards: int) -> np.ndarray:
+    """Contiguous shard bounds with near-equal cumulative block counts."""
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+    bounds = np.zeros(n_shards + 1, dtype=np.uint64)
+    arg = lengths if lengths.size else np.zeros(1, dtype=np.uint64)
+    rc = L.lib().msha_partition_by_blocks(_p(arg, ctypes.c_uint64), lengths.size, n_shards,
+                                          _p(bounds, ctypes.c_uint64))
+    if rc != L.MSHA_OK:
+        raise MshaError(rc, "partition_by_blocks")
+    return bounds
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    L.lib().msha_device_count(ctypes.byref(n))
+    return n.value
+
+
+class Engine:
+    """A libmirsha context on the GPUs in ``device_mask`` (bit i = device i)."""
+
+    def __init__(self, device_mask: int = 1):
+        self._lib = L.lib()
+        ctx = ctypes.c_void_p()
+        rc = self._lib.msha_ctx_create(device_mask, ctypes.byref(ctx))
+        if rc != L.MSHA_OK:
+            raise MshaError(rc, self._lib.msha_last_error(None).decode())
+        self._ctx = ctx
+
+    # -- lifecycle -------------------------------------------------------
+    def close(self) -> None:
+        if getattr(self, "_ctx", None):
+            self._lib.msha_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc: int) -> None:
+        if rc != L.MSHA_OK:
+            raise MshaError(rc, self._lib.msha_last_error(self._ctx).decode())
+
+    def stats(self) -> dict:
+        s = L.MshaStats()
+        self._check(self._lib.msha_get_stats(self._ctx, ctypes.byref(s)))
+        return {name: getattr(s, name) for name, _ in L.MshaStats._fields_}
+
+    # -- host-memory entry points -----------------------------------------
+    def digest_batch(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray) -> np.ndarray:
+        """out[i] = SHA-256(arena[off[i] : off[i]+len[i]]) -> uint8 [n, 32]."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8).reshape(-1)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        length = np.ascontiguousarray(length, dtype=np.uint64)
+        n = off.size
+        out = np.empty((n, 32), dtype=np.uint8)
+        if n == 0:
+            return out
+        ap = arena if arena.size else np.zeros(1, dtype=np.uint8)
+        self._check(self._lib.msha_digest_batch(self._ctx, _p(ap, ctypes.c_uint8), arena.size,
+                                                _p(off, ctypes.c_uint64), _p(length, ctypes.c_uint64),
+                                                n, _p(out, ctypes.c_uint8)))
+        return out
+
+    def hash_actions_packed(self, arena: np.ndarray, part_off: np.ndarray, part_len: np.ndarray,
+                            action_part_begin: np.ndarray) -> np.ndarray:
+        """msha_hash_actions over a packed arena -> uint8 [n_actions, 32]."""
+        arena = np.ascontiguousarray(arena, dtype=np.uint8).reshape(-1)
+        part_off = np.ascontiguousarray(part_off, dtype=np.uint64)
+        part_len = np.ascontiguousarray(part_len, dtype=np.uint64)
+        begin = np.ascontiguousarray(action_part_begin, dtype=np.uint64)
+        n_actions = begin.size - 1
+        out = np.empty((max(n_actions, 0), 32), dtype=np.uint8)
+        if n_actions <= 0:
+            return out
+        ap = arena if arena.size else np.zeros(1, dtype=np.uint8)
+        po = part_off if part_off.size else np.zeros(1, dtype=np.uint64)
+        pl = part_len if part_len.size else np.zeros(1, dtype=np.uint64)
+        self._check(self._lib.msha_hash_actions(self._ctx, _p(ap, ctypes.c_uint8), arena.size,
+                                                _p(po, ctypes.c_uint64), _p(pl, ctypes.c_uint64),
+                                                part_off.size, _p(begin, ctypes.c_uint64), n_actions,
+                                                _p(out, ctypes.c_uint8)))
+        return out
+
+    def hash_actions(self, actions: Sequence[Sequence[bytes]]) -> list[bytes]:
+        """One digest per action = SHA-256(concat(parts)), in input order."""
+        arena, part_off, part_len, begin = pack_parts(actions)
+        out = self.hash_actions_packed(arena, part_off, part_len, begin)
+        return [bytes(r) for r in out]
+
+    def digest_of_digests(self, table: np.ndarray, idx: np.ndarray, begin: np.ndarray) -> np.ndarray:
+        table = np.ascontiguousarray(table, dtype=np.uint8).reshape(-1, 32)
+        idx = np.ascontiguousarray(idx, dtype=np.uint32)
+        begin = np.ascontiguousarray(begin, dtype=np.uint64)
+        n = begin.size - 1
+        out = np.empty((n, 32), dtype=np.uint8)
+        if n <= 0:
+            return out
+        tp = table if table.size else np.zeros((1, 32), dtype=np.uint8)
+        ip = idx if idx.size else np.zeros(1, dtype=np.uint32)
+        self._check(self._lib.msha_digest_of_digests(self._ctx, _p(tp, ctypes.c_uint8), table.shape[0],
+                                                     _p(ip, ctypes.c_uint32), idx.size,
+                                                     _p(begin, ctypes.c_uint64), n,
+                                                     _p(out, ctypes.c_uint8)))
+        return out
+
+    # -- device-resident entry points (torch tensors on the GPU) ----------
+    @staticmethod
+    def _stream_ptr(stream) -> Optional[int]:
+        if stream is None:
+            return None
+        return int(getattr(stream, "cuda_stream", stream))
+
+    def digest_batch_device(self, arena, off, length, out, stream=None) -> None:
+        self._check(self._lib.msha_digest_batch_device(self._ctx, arena.data_ptr(), off.data_ptr(),
+                                                       length.data_ptr(), off.numel(), out.data_ptr(),
+                                                       self._stream_ptr(stream)))
+
+    def digest_uniform_device(self, arena, stride: int, msg_len: int, n: int, out, stream=None) -> None:
+        self._check(self._lib.msha_digest_uniform_device(self._ctx, arena.data_ptr(), stride, msg_len, n,
+                                                         out.data_ptr(), self._stream_ptr(stream)))
+
+    def digest_of_digests_device(self, table, idx, begin, out, stream=None) -> None:
+        self._check(self._lib.msha_digest_of_digests_device(self._ctx, table.data_ptr(), idx.data_ptr(),
+                                                            begin.data_ptr(), begin.numel() - 1,
+                                                            out.data_ptr(), self._stream_ptr(stream)))
+
+    def device_status(self) -> None:
+        self._check(self._lib.msha_device_status(self._ctx))
+
+
+def pack_parts(actions: Sequence[Sequence[bytes]]):
+    """Pack [][]byte parts into (arena, part_off, part_len, action_part_begin),
+    the layout a cgo adapter hands to msha_hash_actions."""
+    parts = [bytes(p) for a in actions for p in a]
+    lens = np.fromiter((len(p) for p in parts), dtype=np.uint64, count=len(parts))
+    offs = np.zeros(len(parts), dtype=np.uint64)
+    if len(parts) > 1:
+        offs[1:] = np.cumsum(lens)[:-1]
+    arena = np.frombuffer(b"".join(parts), dtype=np.uint8)
+    begin = np.zeros(len(actions) + 1, dtype=np.uint64)
+    if actions:
+        begin[1:] = np.cumsum([len(a) for a in actions])
+    return arena, offs, lens, begin

@@ -1,0 +1,202 @@
+"""Host-side mirror of the reference's hash plugin surface, backed by the GPU.
+
+Reference interface (Go, /root/reference/pkg/processor/serial.go):
+
+    type Hasher interface { New() hash.Hash }                              // :21-23
+    func ProcessHashActions(hasher Hasher, actions *statemachine.ActionList)
+            (*statemachine.EventList, error)                               // :180-198
+
+with the action/event constructors of pkg/statemachine/actions.go:173-187 and
+events.go:96-110 and the schema of protos/state/state.proto:78-109,168-171.
+
+Names, argument meaning and error behaviour follow the reference:
+``ProcessHashActions`` returns one ``HashResult`` per action, in list order,
+whose ``origin`` is the *same object* as the action's; a non-hash action makes
+it fail with "unexpected type for Hash action: <type>" (serial.go:192-194),
+raised here as ``ProcessorError``. The whole list is hashed by ONE
+``msha_hash_actions`` call (one H2D, one launch per GPU, one D2H).
+
+``GPUHasher.new()`` keeps the per-message ``hash.Hash`` surface that
+``Client.Propose`` (clients.go:189-192) and the testengine app chain
+(recorder.go:288-359) use: writes are buffered and ``sum()`` submits a
+one-message batch to the GPU. Nothing in this module hashes on the CPU.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import Any, Iterator, List, Optional, Sequence, Union
+
+from .encoding import EpochChange, RequestAck
+from .engine import Engine
+
+
+class ProcessorError(RuntimeError):
+    pass
+
+
+# ---------------------------------------------------------------------------
+# state.HashOrigin and friends (protos/state/state.proto:78-104)
+# ---------------------------------------------------------------------------
+@dataclass
+class HashOriginBatch:
+    source: int
+    epoch: int
+    seq_no: int
+    request_acks: List[RequestAck] = field(default_factory=list)
+
+
+@dataclass
+class HashOriginVerifyBatch:
+    source: int
+    seq_no: int
+    request_acks: List[RequestAck] = field(default_factory=list)
+    expected_digest: bytes = b""
+
+
+@dataclass
+class HashOriginEpochChange:
+    source: int
+    origin: int
+    epoch_change: Optional[EpochChange] = None
+
+
+@dataclass
+class HashOrigin:
+    type: Union[HashOriginBatch, HashOriginVerifyBatch, HashOriginEpochChange, None] = None
+
+
+@dataclass
+class ActionHashRequest:
+    """state.ActionHashRequest{repeated bytes data; HashOrigin origin} (state.proto:168-171)."""
+    data: List[bytes]
+    origin: Optional[HashOrigin]
+
+
+@dataclass
+class ActionHash:
+    hash: ActionHashRequest
+
+
+@dataclass
+class Action:
+    """state.Action: a oneof; only ActionHash is valid on the hash path."""
+    type: Any
+
+
+@dataclass
+class EventHashResult:
+    """state.EventHashResult{bytes digest; HashOrigin origin} (state.proto:106-109)."""
+    digest: bytes
+    origin: Optional[HashOrigin]
+
+
+@dataclass
+class EventHashResultType:
+    hash_result: EventHashResult
+
+
+@dataclass
+class Event:
+    type: Any
+
+
+class ActionList:
+    """statemachine.ActionList (a linked list in Go; order is what matters)."""
+
+    def __init__(self, actions: Optional[Sequence[Action]] = None):
+        self._l: List[Action] = list(actions or [])
+
+    def push_back(self, a: Action) -> "ActionList":
+        self._l.append(a)
+        return self
+
+    def hash(self, data: List[bytes], origin: Optional[HashOrigin]) -> "ActionList":
+        """ActionList.Hash (actions.go:173-176)."""
+        return self.push_back(action_hash(data, origin))
+
+    def __iter__(self) -> Iterator[Action]:
+        return iter(self._l)
+
+    def __len__(self) -> int:
+        return len(self._l)
+
+
+class EventList:
+    def __init__(self):
+        self._l: List[Event] = []
+
+    def push_back(self, e: Event) -> "EventList":
+        self._l.append(e)
+        return self
+
+    def hash_result(self, digest: bytes, origin: Optional[HashOrigin]) -> "EventList":
+        """EventList.HashResult (events.go:96-99)."""
+        return self.push_back(Event(EventHashResultType(EventHashResult(digest, origin))))
+
+    def __iter__(self) -> Iterator[Event]:
+        return iter(self._l)
+
+    def __len__(self) -> int:
+        return len(self._l)
+
+
+def action_hash(data: List[bytes], origin: Optional[HashOrigin]) -> Action:
+    """statemachine.ActionHash (actions.go:178-187)."""
+    return Action(ActionHash(ActionHashRequest(data=list(data), origin=origin)))
+
+
+# ---------------------------------------------------------------------------
+# Hasher
+# ---------------------------------------------------------------------------
+class _GPUHash:
+    """hash.Hash over the GPU engine: Write appends, Sum(b) appends the digest
+    of everything written so far without resetting (Go hash.Hash semantics)."""
+
+    size = 32
+    block_size = 64
+
+    def __init__(self, engine: Engine):
+        self._engine = engine
+        self._buf = bytearray()
+
+    def write(self, p: bytes) -> int:
+        self._buf += p
+        return len(p)
+
+    def sum(self, b: bytes = b"") -> bytes:
+        return bytes(b) + self._engine.hash_actions([[bytes(self._buf)]])[0]
+
+    def reset(self) -> None:
+        self._buf.clear()
+
+
+class GPUHasher:
+    """processor.Hasher backed by libmirsha; also exposes the batched surface
+    ProcessHashActions uses."""
+
+    def __init__(self, engine: Optional[Engine] = None, device_mask: int = 1):
+        self.engine = engine if engine is not None else Engine(device_mask)
+
+    def new(self) -> _GPUHash:
+        return _GPUHash(self.engine)
+
+    def hash_batch(self, actions: Sequence[Sequence[bytes]]) -> List[bytes]:
+        return self.engine.hash_actions(actions)
+
+
+def ProcessHashActions(hasher: GPUHasher, actions: ActionList) -> EventList:
+    """processor.ProcessHashActions (serial.go:180-198), one GPU batch per list."""
+    if not hasattr(hasher, "hash_batch"):
+        raise TypeError("ProcessHashActions needs a GPU-backed hasher (GPUHasher); "
+                        "this engine has no CPU hashing path")
+    reqs: List[ActionHashRequest] = []
+    for action in actions:
+        t = action.type
+        if not isinstance(t, ActionHash):
+            raise ProcessorError(f"unexpected type for Hash action: {type(t).__name__}")
+        reqs.append(t.hash)
+    digests = hasher.hash_batch([r.data for r in reqs]) if reqs else []
+    events = EventList()
+    for r, d in zip(reqs, digests):
+        events.hash_result(d, r.origin)
+    return events

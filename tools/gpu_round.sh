@@ -1,0 +1,29 @@
+#!/bin/bash
+# One GPU-box session: parity tests, smoke, bench lines per config, rocprofv3 kernel stats.
+# Every GPU step has its own time limit; a fault/abort/timeout ends the session.
+set -u
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+stop_on_fault() { local rc=$1 name=$2; echo "$name rc=$rc"; if [ $rc -ge 124 ]; then echo "FAULT/TIMEOUT in $name: stopping"; exit $rc; fi; }
+STEPS=${STEPS:-all}
+if [[ $STEPS == all || $STEPS == *tests* ]]; then
+  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; stop_on_fault $? pytest
+  tail -5 gpurun_out/pytest_gpu.log
+fi
+if [[ $STEPS == all || $STEPS == *smoke* ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1; stop_on_fault $? smoke
+  tail -2 gpurun_out/smoke.log
+fi
+if [[ $STEPS == all || $STEPS == *bench* ]]; then
+  for cfg in ${CONFIGS:-c2 c3 c3dd c4 c5}; do
+    extra="--no-cpu-baseline"; [ $cfg == c2 ] && extra=""
+    timeout -k 10 400 python bench.py --config $cfg --steps ${BSTEPS:-10} $extra > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err; stop_on_fault $? bench_$cfg
+    cat gpurun_out/bench_$cfg.json
+  done
+fi
+if [[ $STEPS == all || $STEPS == *prof* ]]; then
+  rm -rf gpurun_out/prof
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --config ${PCFG:-c2} --steps 10 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1; stop_on_fault $? rocprof
+  find gpurun_out/prof -name "*kernel_stats*" | head -3
+  for f in $(find gpurun_out/prof -name "*kernel_stats.csv"); do cat $f; done
+fi
