@@ -131,8 +131,14 @@ def main():
         def step():
             eng.digest_of_digests_device(d_table, d_idx, d_begin, d_out, stream)
     else:
+        d_order = None
+        if not w.uniform_stride:
+            # mixed sizes: the packer's size-class order (host, once; part of packing)
+            from mirbft_amd.engine import order_by_blocks
+            d_order = torch.from_numpy(order_by_blocks(w.len).view(np.int32)).to(dev)
+
         def step():
-            eng.digest_batch_device(d_arena, d_off, d_len, d_out, stream)
+            eng.digest_batch_device(d_arena, d_off, d_len, d_out, stream, order=d_order)
 
     for _ in range(args.warmup):
         step()

@@ -126,10 +126,14 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
  * stream); the call returns after enqueueing. Arena rules: message starts
  * MSHA_DEVICE_ALIGN-aligned, MSHA_DEVICE_ARENA_SLACK readable bytes after the
  * last message. A misaligned start is reported by msha_device_status() and its
- * digest is zeroed (never a wrong digest).
+ * digest is zeroed (never a wrong digest). d_order (may be NULL) is a
+ * permutation of [0, n): lane i hashes message d_order[i] (digest still lands
+ * at d_out + 32*d_order[i]); pass msha_order_by_blocks()'s output for batches
+ * of mixed sizes so every wavefront's lanes run the same number of blocks.
  */
 int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
-                             const uint64_t* d_len, uint64_t n, uint8_t* d_out, void* stream);
+                             const uint64_t* d_len, const uint32_t* d_order, uint64_t n,
+                             uint8_t* d_out, void* stream);
 int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t stride,
                                uint64_t msg_len, uint64_t n, uint8_t* d_out, void* stream);
 int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const uint32_t* d_idx,
@@ -152,6 +156,8 @@ int msha_pinned_free(msha_ctx* ctx, void* p);
  *   (bounds[0] = 0, bounds[n_shards] = n). Used for multi-GPU sharding.
  */
 uint64_t msha_blocks_for_len(uint64_t len);
+/* Permutation of [0, n) ordering messages by descending block count (stable). */
+int msha_order_by_blocks(const uint64_t* len, uint64_t n, uint32_t* order);
 int msha_partition_by_blocks(const uint64_t* len, uint64_t n, uint32_t n_shards,
                              uint64_t* bounds);
 

@@ -57,7 +57,8 @@ SIGNATURES = {
     "msha_digest_of_digests": (ctypes.c_int, [_ctxp, _u8p, ctypes.c_uint64, _u32p, ctypes.c_uint64,
                                               _u64p, ctypes.c_uint64, _u8p]),
     "msha_digest_batch_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                                ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
+                                                ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                                ctypes.c_void_p]),
     "msha_digest_uniform_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     "msha_digest_of_digests_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_void_p,
@@ -67,6 +68,7 @@ SIGNATURES = {
     "msha_pinned_alloc": (ctypes.c_int, [_ctxp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "msha_pinned_free": (ctypes.c_int, [_ctxp, ctypes.c_void_p]),
     "msha_blocks_for_len": (ctypes.c_uint64, [ctypes.c_uint64]),
+    "msha_order_by_blocks": (ctypes.c_int, [_u64p, ctypes.c_uint64, _u32p]),
     "msha_partition_by_blocks": (ctypes.c_int, [_u64p, ctypes.c_uint64, ctypes.c_uint32, _u64p]),
 }
 

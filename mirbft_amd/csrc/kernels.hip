@@ -15,6 +15,7 @@
 //   out    : 32 bytes per message, digest i at out + 32*i
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "sha256_device.hpp"
 #include "kernels.hpp"
@@ -36,30 +37,61 @@ __device__ __forceinline__ void to_words(const uint32_t (&raw)[16], uint32_t (&w
   for (int j = 0; j < 16; ++j) w[j] = bswap(raw[j]);
 }
 
+// How a lane brings its message blocks in from HBM (all modes are bit-identical):
+//  kSingle   load block b at the top of iteration b; latency hidden by the
+//            other waves of the SIMD (high occupancy)
+//  kPrefetch load block b+1 while block b is compressed (16 more live VGPRs):
+//            for few, long messages, where there are too few waves to hide it
+//  kPair     at even b load blocks b and b+1 together: both halves of a
+//            128-byte line are requested back to back, so the line is read
+//            from HBM once instead of being evicted and re-fetched between
+//            the two half-line requests (lane stride >= 128 B is the norm)
+enum LoadMode { kSingle = 0, kPrefetch = 1, kPair = 2 };
+
 // Hash one message of `len` bytes starting at p (device memory, 16-byte
 // aligned, with kArenaSlack (kernels.hpp) readable bytes after the arena's last
 // message) into out. One compress() call site: full blocks, the tail block
 // and the optional extra length block all go through the same loop body.
 // The tail block is read as a whole 64-byte block (it may run into the next
 // message or the slack); build_tail() masks every byte at or past `len`.
-// PREFETCH=true loads block b+1 while block b is compressed (16 more VGPRs):
-// used when there are too few waves per SIMD to hide HBM latency by
-// occupancy (few, long messages).
-template <bool PREFETCH>
+template <int MODE>
 __device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uint8_t* out) {
   State s;
   state_init(s);
   const uint32_t nfull = (uint32_t)(len >> 6);  // < 2^32 blocks: messages < 256 GiB
   const uint32_t r = (uint32_t)(len & 63);
   const uint32_t nblocks = nfull + (r < 56 ? 1 : 2);
+  // Wave-uniform length (the common batch shape: request digests, Batch
+  // digests, large payloads) whose last block carries no message byte: that
+  // block goes to compress_uniform_pad() (schedule on the SALU) after the loop.
+  const uint32_t len_lo0 = __builtin_amdgcn_readfirstlane((uint32_t)len);
+  const uint32_t len_hi0 = __builtin_amdgcn_readfirstlane((uint32_t)(len >> 32));
+  const uint64_t len0 = ((uint64_t)len_hi0 << 32) | len_lo0;
+  const bool uniform = __ballot(len != len0) == 0;
+  const uint32_t r0 = len_lo0 & 63;
+  const bool upad = uniform && (r0 == 0 || r0 >= 56);
+  const uint32_t nvalu = nblocks - (upad ? 1 : 0);
   uint32_t raw[16];
   uint32_t w[16];
-  if (PREFETCH) load_block16(p, raw);
-  for (uint32_t b = 0; b < nblocks; ++b) {
-    if (!PREFETCH && b <= nfull) load_block16(p + 64 * (uint64_t)b, raw);
+  if (MODE == kPrefetch) load_block16(p, raw);
+  for (uint32_t b = 0; b < nvalu; ++b) {
+    const uint8_t* pb = p + 64 * (uint64_t)b;
+    if (MODE == kSingle && b <= nfull) load_block16(pb, raw);
+    if (MODE == kPair && b == nfull && !(b & 1)) load_block16(pb, raw);
     if (b < nfull) {
-      to_words(raw, w);
-      if (PREFETCH) load_block16(p + 64 * (uint64_t)(b + 1), raw);
+      if (MODE == kPair) {
+        if (!(b & 1)) {
+          uint32_t t[16];
+          load_block16(pb, t);
+          load_block16(pb + 64, raw);  // block b+1, or the tail block's bytes (slack-safe)
+          to_words(t, w);
+        } else {
+          to_words(raw, w);
+        }
+      } else {
+        to_words(raw, w);
+        if (MODE == kPrefetch) load_block16(pb + 64, raw);
+      }
     } else if (b == nfull) {
       // Launder r so the 16 per-dword tail masks are built here, once, and
       // not hoisted out of the loop into 32 loop-long VGPRs.
@@ -70,6 +102,10 @@ __device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uin
       length_block(len, w);
     }
     compress(s, w);
+  }
+  if (upad) {
+    const uint64_t bits = len0 * 8;
+    compress_uniform_pad(s, r0 == 0 ? 0x80000000u : 0u, (uint32_t)(bits >> 32), (uint32_t)bits);
   }
   store_digest(s, out);
 }
@@ -84,7 +120,7 @@ __device__ __forceinline__ bool check_aligned(const uint8_t* p, uint8_t* out, ui
   return false;
 }
 
-template <bool PREFETCH>
+template <int MODE>
 __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restrict__ arena,
                                                       const uint64_t* __restrict__ off,
                                                       const uint64_t* __restrict__ len,
@@ -95,11 +131,11 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
   if (i >= n) return;
   const uint64_t m = order ? (uint64_t)order[i] : i;
   const uint8_t* p = arena + off[m];
-  if (check_aligned(p, out + 32 * m, err)) hash_message<PREFETCH>(p, len[m], out + 32 * m);
+  if (check_aligned(p, out + 32 * m, err)) hash_message<MODE>(p, len[m], out + 32 * m);
 }
 
 // Uniform layout: message i is arena[i*stride : i*stride + msg_len].
-template <bool PREFETCH>
+template <int MODE>
 __global__ __launch_bounds__(256, 8) void k_digest_uniform(const uint8_t* __restrict__ arena,
                                                         uint64_t stride, uint64_t msg_len,
                                                         uint64_t n, uint8_t* __restrict__ out,
@@ -107,7 +143,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_uniform(const uint8_t* __rest
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* p = arena + i * stride;
-  if (check_aligned(p, out + 32 * i, err)) hash_message<PREFETCH>(p, msg_len, out + 32 * i);
+  if (check_aligned(p, out + 32 * i, err)) hash_message<MODE>(p, msg_len, out + 32 * i);
 }
 
 // Digest-of-digests (Batch / VerifyBatch actions, /root/reference/pkg/statemachine/
@@ -164,19 +200,34 @@ __global__ __launch_bounds__(256, 8) void k_digest_of_digests(const uint8_t* __r
 static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 // Fewer than ~3 waves per SIMD cannot hide HBM latency by occupancy: use the
-// register-prefetching variant then.
-static inline bool want_prefetch(uint64_t n, int cus) { return n < (uint64_t)cus * 4 * 64 * 3; }
+// register-prefetching variant then; otherwise pair loads. MSHA_LOAD_MODE
+// (0/1/2) overrides, for A/B measurements.
+static inline int pick_mode(uint64_t n, int cus) {
+  static const int forced = [] {
+    const char* e = getenv("MSHA_LOAD_MODE");
+    return e ? atoi(e) : -1;
+  }();
+  if (forced >= 0 && forced <= 2) return forced;
+  return n < (uint64_t)cus * 4 * 64 * 3 ? kPrefetch : kPair;
+}
 
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
                                const uint32_t* order, uint64_t n, uint8_t* out, uint32_t* err,
                                int cus, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (want_prefetch(n, cus))
-    hipLaunchKernelGGL(k_digest_batch<true>, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
-                       order, n, out, err);
-  else
-    hipLaunchKernelGGL(k_digest_batch<false>, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
-                       order, n, out, err);
+  switch (pick_mode(n, cus)) {
+    case kSingle:
+      hipLaunchKernelGGL(k_digest_batch<kSingle>, dim3(grid_for(n)), dim3(256), 0, st, arena, off,
+                         len, order, n, out, err);
+      break;
+    case kPrefetch:
+      hipLaunchKernelGGL(k_digest_batch<kPrefetch>, dim3(grid_for(n)), dim3(256), 0, st, arena, off,
+                         len, order, n, out, err);
+      break;
+    default:
+      hipLaunchKernelGGL(k_digest_batch<kPair>, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
+                         order, n, out, err);
+  }
   return hipGetLastError();
 }
 
@@ -184,12 +235,19 @@ hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st) {
   if (n == 0) return hipSuccess;
-  if (want_prefetch(n, cus))
-    hipLaunchKernelGGL(k_digest_uniform<true>, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
-                       msg_len, n, out, err);
-  else
-    hipLaunchKernelGGL(k_digest_uniform<false>, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
-                       msg_len, n, out, err);
+  switch (pick_mode(n, cus)) {
+    case kSingle:
+      hipLaunchKernelGGL(k_digest_uniform<kSingle>, dim3(grid_for(n)), dim3(256), 0, st, arena,
+                         stride, msg_len, n, out, err);
+      break;
+    case kPrefetch:
+      hipLaunchKernelGGL(k_digest_uniform<kPrefetch>, dim3(grid_for(n)), dim3(256), 0, st, arena,
+                         stride, msg_len, n, out, err);
+      break;
+    default:
+      hipLaunchKernelGGL(k_digest_uniform<kPair>, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
+                         msg_len, n, out, err);
+  }
   return hipGetLastError();
 }
 

@@ -345,6 +345,18 @@ int msha_get_stats(const msha_ctx* ctx, msha_stats* out) {
 
 uint64_t msha_blocks_for_len(uint64_t len) { return blocks_for(len); }
 
+int msha_order_by_blocks(const uint64_t* len, uint64_t n, uint32_t* order) {
+  if (n && (!len || !order)) return MSHA_ERR_INVALID_ARG;
+  if (n > 0xffffffffull) return MSHA_ERR_INVALID_ARG;
+  try {
+    std::vector<uint32_t> tmp;
+    order_by_blocks_desc(len, n, order, tmp);
+  } catch (...) {
+    return MSHA_ERR_OUT_OF_MEMORY;
+  }
+  return MSHA_OK;
+}
+
 int msha_partition_by_blocks(const uint64_t* len, uint64_t n, uint32_t n_shards, uint64_t* bounds) {
   if (!bounds || n_shards == 0 || (n && !len)) return MSHA_ERR_INVALID_ARG;
   partition(len, n, n_shards, bounds);
@@ -546,7 +558,8 @@ static int device_prologue(msha_ctx* ctx, void* stream, hipStream_t* st) {
 }
 
 int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
-                             const uint64_t* d_len, uint64_t n, uint8_t* d_out, void* stream) {
+                             const uint64_t* d_len, const uint32_t* d_order, uint64_t n,
+                             uint8_t* d_out, void* stream) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n == 0) return MSHA_OK;
   if (!d_arena || !d_off || !d_len || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
@@ -554,7 +567,7 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
     hipStream_t st;
     device_prologue(ctx, stream, &st);
     Device& d = ctx->devs[0];
-    HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, nullptr, n, d_out, d.err.as<uint32_t>(),
+    HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, d_order, n, d_out, d.err.as<uint32_t>(),
                                      d.cus, st));
   });
 }

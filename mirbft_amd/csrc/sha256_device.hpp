@@ -107,6 +107,72 @@ __device__ __forceinline__ void compress(State& s, uint32_t (&w)[16]) {
   s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
 }
 
+// ---- scalar-unit (SALU) helpers for wave-uniform values -------------------
+// SALU has no rotate; LLVM would turn a shift/or rotate back into the VALU
+// v_alignbit_b32, so the scalar rotate is spelled out in asm.
+template <int N>
+__device__ __forceinline__ uint32_t srotr(uint32_t x) {
+  uint32_t r, t;
+  asm("s_lshr_b32 %0, %2, %3\n\ts_lshl_b32 %1, %2, %4\n\ts_or_b32 %0, %0, %1"
+      : "=&s"(r), "=&s"(t)
+      : "s"(x), "i"(N), "i"(32 - N)
+      : "scc");
+  return r;
+}
+__device__ __forceinline__ uint32_t ssig0(uint32_t x) { return srotr<7>(x) ^ srotr<18>(x) ^ (x >> 3); }
+__device__ __forceinline__ uint32_t ssig1(uint32_t x) { return srotr<17>(x) ^ srotr<19>(x) ^ (x >> 10); }
+
+// Compress a final block whose words are all wave-uniform: the padding-only
+// block of a message with len % 64 == 0 (w0 = 0x80000000) or the length-only
+// block after a tail of >= 56 bytes (w0 = 0). Its 48-word schedule depends
+// only on the length, so it is expanded once per wave on the scalar unit and
+// every round takes K[t]+W[t] from an SGPR: the VALU does only the 64 rounds.
+__device__ __forceinline__ void compress_uniform_pad(State& s, uint32_t w0, uint32_t bits_hi,
+                                                     uint32_t bits_lo) {
+  constexpr uint32_t K[64] = {MSHA_K_TABLE};
+  uint32_t w[16];
+  w[0] = w0;
+#pragma unroll
+  for (int j = 1; j < 14; ++j) w[j] = 0;
+  w[14] = bits_hi;
+  w[15] = bits_lo;
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+  uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#define MSHA_W_UDIRECT(i) w[(i) & 15]
+#define MSHA_W_USCHED(i) \
+  (w[(i) & 15] += ssig1(w[((i) - 2) & 15]) + w[((i) - 7) & 15] + ssig0(w[((i) - 15) & 15]))
+#define MSHA_UROUND(a, b, c, d, e, f, g, h, i, W)           \
+  {                                                         \
+    const uint32_t kw = K[i] + W(i); /* SALU */             \
+    uint32_t t1 = h + kw + Sig1(e) + ch(e, f, g);           \
+    d += t1;                                                \
+    h = t1 + Sig0(a) + maj(a, b, c);                        \
+  }
+#define MSHA_UR8(i, W)                              \
+  MSHA_UROUND(a, b, c, d, e, f, g, h, (i) + 0, W)   \
+  MSHA_UROUND(h, a, b, c, d, e, f, g, (i) + 1, W)   \
+  MSHA_UROUND(g, h, a, b, c, d, e, f, (i) + 2, W)   \
+  MSHA_UROUND(f, g, h, a, b, c, d, e, (i) + 3, W)   \
+  MSHA_UROUND(e, f, g, h, a, b, c, d, (i) + 4, W)   \
+  MSHA_UROUND(d, e, f, g, h, a, b, c, (i) + 5, W)   \
+  MSHA_UROUND(c, d, e, f, g, h, a, b, (i) + 6, W)   \
+  MSHA_UROUND(b, c, d, e, f, g, h, a, (i) + 7, W)
+  MSHA_UR8(0, MSHA_W_UDIRECT)
+  MSHA_UR8(8, MSHA_W_UDIRECT)
+  MSHA_UR8(16, MSHA_W_USCHED)
+  MSHA_UR8(24, MSHA_W_USCHED)
+  MSHA_UR8(32, MSHA_W_USCHED)
+  MSHA_UR8(40, MSHA_W_USCHED)
+  MSHA_UR8(48, MSHA_W_USCHED)
+  MSHA_UR8(56, MSHA_W_USCHED)
+#undef MSHA_UR8
+#undef MSHA_UROUND
+#undef MSHA_W_USCHED
+#undef MSHA_W_UDIRECT
+  s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+  s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
 // Words of the final (padded) block(s), built from the r = len % 64 leftover
 // bytes whose little-endian dwords are raw[0..15] (dwords at or past r are
 // ignored). Returns 1 if a second, all-padding block is needed (r >= 56).

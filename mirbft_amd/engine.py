@@ -42,6 +42,17 @@ def partition_by_blocks(lengths: np.ndarray, n_shards: int) -> np.ndarray:
     return bounds
 
 
+def order_by_blocks(lengths: np.ndarray) -> np.ndarray:
+    """Permutation ordering messages by descending block count (for d_order)."""
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint64)
+    order = np.zeros(max(lengths.size, 1), dtype=np.uint32)
+    arg = lengths if lengths.size else np.zeros(1, dtype=np.uint64)
+    rc = L.lib().msha_order_by_blocks(_p(arg, ctypes.c_uint64), lengths.size, _p(order, ctypes.c_uint32))
+    if rc != L.MSHA_OK:
+        raise MshaError(rc, "order_by_blocks")
+    return order[: lengths.size]
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     L.lib().msha_device_count(ctypes.byref(n))
@@ -151,10 +162,11 @@ class Engine:
             return None
         return int(getattr(stream, "cuda_stream", stream))
 
-    def digest_batch_device(self, arena, off, length, out, stream=None) -> None:
+    def digest_batch_device(self, arena, off, length, out, stream=None, order=None) -> None:
         self._check(self._lib.msha_digest_batch_device(self._ctx, arena.data_ptr(), off.data_ptr(),
-                                                       length.data_ptr(), off.numel(), out.data_ptr(),
-                                                       self._stream_ptr(stream)))
+                                                       length.data_ptr(),
+                                                       None if order is None else order.data_ptr(),
+                                                       off.numel(), out.data_ptr(), self._stream_ptr(stream)))
 
     def digest_uniform_device(self, arena, stride: int, msg_len: int, n: int, out, stream=None) -> None:
         self._check(self._lib.msha_digest_uniform_device(self._ctx, arena.data_ptr(), stride, msg_len, n,

@@ -77,3 +77,18 @@ def test_null_args_rejected_without_gpu():
     assert lib.msha_get_stats(None, None) == L.MSHA_ERR_INVALID_ARG
     assert lib.msha_digest_batch(None, None, 0, None, None, 0, None) == L.MSHA_ERR_INVALID_ARG
     assert lib.msha_partition_by_blocks(None, 1, 1, None) == L.MSHA_ERR_INVALID_ARG
+
+
+def test_order_by_blocks_is_descending_stable_permutation():
+    from mirbft_amd.engine import order_by_blocks
+    rng = np.random.default_rng(1)
+    lens = rng.integers(0, 5000, 20_000).astype(np.uint64)
+    o = order_by_blocks(lens)
+    assert sorted(o.tolist()) == list(range(lens.size))
+    b = np.array([blocks_for_len(int(x)) for x in lens])[o]
+    assert np.all(np.diff(b) <= 0)
+    # stable: equal block counts keep index order
+    for v in np.unique(b)[:5]:
+        idx = o[b == v]
+        assert np.all(np.diff(idx.astype(np.int64)) > 0)
+    assert order_by_blocks(np.zeros(0, dtype=np.uint64)).size == 0

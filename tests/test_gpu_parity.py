@@ -292,3 +292,16 @@ def test_c5_sample_mixed(engine):
 def test_pack_parts_layout():
     arena, po, pl, b = pack_parts([[b"ab", b""], [], [b"c"]])
     assert arena.tobytes() == b"abc" and list(pl) == [2, 0, 1] and list(b) == [0, 2, 2, 3]
+
+
+def test_c5_device_ordered(engine):
+    """Mixed sizes through the device path with the size-class order (bench c5 form)."""
+    import torch
+    from mirbft_amd.engine import order_by_blocks
+    w = W.c5_storm(1 << 16)
+    d_arena, d_off, d_len = _to_dev(w)
+    d_order = torch.from_numpy(order_by_blocks(w.len).view(np.int32)).to("cuda:0")
+    out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device(d_arena, d_off, d_len, out, order=d_order)
+    engine.device_status()
+    assert np.array_equal(out.cpu().numpy(), oracle.digest_batch(w.arena, w.off, w.len))
