@@ -1,0 +1,108 @@
+// C++ parity test for the reference-shaped host mirror (include/mirbft/processor.hpp).
+// Reads like the reference's ginkgo specs for the processor: Describe
+// ProcessHashActions -> It "..." -> Expect. The checker is the CPU oracle
+// (oracle/sha256_oracle.c, linked as test infrastructure only).
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+
+#include "mirbft/processor.hpp"
+
+extern "C" void oracle_sha256(const uint8_t* p, uint64_t n, uint8_t out[32]);
+
+using namespace mirbft;
+using mirbft::statemachine::ActionList;
+
+static int failures = 0;
+#define EXPECT(cond, what)                                                  \
+  do {                                                                      \
+    if (!(cond)) {                                                          \
+      std::fprintf(stderr, "FAIL %s:%d: %s\n", __FILE__, __LINE__, what);   \
+      ++failures;                                                           \
+    }                                                                       \
+  } while (0)
+
+static Bytes hex(const char* h) {
+  Bytes b;
+  for (size_t i = 0; h[i] && h[i + 1]; i += 2) b.push_back((uint8_t)std::stoi(std::string(h + i, 2), nullptr, 16));
+  return b;
+}
+static Bytes str(const char* s) { return Bytes(s, s + std::strlen(s)); }
+static Bytes oracle(const std::vector<Bytes>& parts) {
+  Bytes all;
+  for (auto& p : parts) all.insert(all.end(), p.begin(), p.end());
+  Bytes d(32);
+  oracle_sha256(all.data(), all.size(), d.data());
+  return d;
+}
+
+int main() {
+  processor::GPUHasher hasher(1);
+
+  // Describe("ProcessHashActions")
+  {  // It("hashes the FIPS 180-4 examples")
+    ActionList al;
+    al.Hash({}, nullptr);
+    al.Hash({str("abc")}, nullptr);
+    al.Hash({str("abcdbcdecdefdefgefghfghighijhijkijkljklmklmnlmnomnopnopq")}, nullptr);
+    auto r = processor::ProcessHashActions(hasher, al);
+    EXPECT(r.ok(), "no error");
+    EXPECT(r.value.Len() == 3, "one result per action");
+    EXPECT(r.value.Items()[0].digest == hex("e3b0c44298fc1c149afbf4c8996fb92427ae41e4649b934ca495991b7852b855"), "empty");
+    EXPECT(r.value.Items()[1].digest == hex("ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"), "abc");
+    EXPECT(r.value.Items()[2].digest == hex("248d6a61d20638b8e5c026930c3e6039a33ce45964ff2167f6ecedd419db06c1"), "448-bit");
+  }
+  {  // It("streams parts like h.Write and keeps order and origin identity")
+    std::mt19937_64 rng(42);
+    ActionList al;
+    std::vector<std::shared_ptr<HashOrigin>> origins;
+    std::vector<std::vector<Bytes>> parts_of;
+    for (int i = 0; i < 2000; ++i) {
+      auto o = std::make_shared<HashOrigin>();
+      o->type = HashOriginBatch{0, 1, (uint64_t)i, {}};
+      std::vector<Bytes> parts(rng() % 6);
+      for (auto& p : parts) {
+        p.resize(rng() % 300);
+        for (auto& c : p) c = (uint8_t)rng();
+      }
+      origins.push_back(o);
+      parts_of.push_back(parts);
+      al.Hash(parts, o);
+    }
+    auto r = processor::ProcessHashActions(hasher, al);
+    EXPECT(r.ok(), "no error");
+    EXPECT(r.value.Len() == 2000, "one result per action");
+    for (int i = 0; i < 2000 && i < (int)r.value.Len(); ++i) {
+      EXPECT(r.value.Items()[i].origin.get() == origins[i].get(), "same origin pointer");
+      EXPECT(r.value.Items()[i].digest == oracle(parts_of[i]), "digest == oracle");
+    }
+  }
+  {  // It("fails on a non-hash action with the reference's message")
+    ActionList al;
+    al.Hash({str("x")}, nullptr);
+    al.PushBack(Action{ActionOther{"*state.Action_Send"}});
+    auto r = processor::ProcessHashActions(hasher, al);
+    EXPECT(!r.ok(), "error returned");
+    EXPECT(r.err == "unexpected type for Hash action: *state.Action_Send", "error text");
+  }
+  {  // It("returns an empty list for an empty list")
+    auto r = processor::ProcessHashActions(hasher, ActionList{});
+    EXPECT(r.ok() && r.value.Len() == 0, "empty");
+  }
+  {  // Describe("GPUHash") It("appends on Sum and does not reset")
+    auto h = hasher.New();
+    h.Write(str("ab"));
+    h.Write(str("c"));
+    EXPECT(h.Sum() == hex("ba7816bf8f01cfea414140de5dae2223b00361a396177a9cb410ff61f20015ad"), "abc");
+    Bytes pre = str("pre");
+    Bytes s = h.Sum(pre);
+    EXPECT(s.size() == 35 && Bytes(s.begin(), s.begin() + 3) == pre, "Sum(b) appends");
+  }
+  if (failures) {
+    std::fprintf(stderr, "%d failure(s)\n", failures);
+    return 1;
+  }
+  std::printf("cpp processor mirror: all specs passed\n");
+  return 0;
+}

@@ -1,0 +1,70 @@
+"""Multi-rank sharding on CPU (gloo, world size 2): each rank builds its own
+disjoint slice of the workload exactly as bench.py does, with no data-path
+collective; together the slices equal the single-process workload."""
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from mirbft_amd import workloads as W
+    # bench.py's slicing: c2 -> first = rank * n ; c5 -> first = rank * (total // world)
+    n = 4096
+    c2 = W.c2_requests(n=n, first=rank * n)
+    c5 = W.c5_storm(n=8192 // world, first=rank * (8192 // world))
+    # the only collective: the harness max-reduce of elapsed time (here a dummy value)
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    q.put((rank, c2.arena[: n * 512].tobytes(), c5.len.copy(), float(t.item())))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_slices_cover_the_global_workload():
+    import torch.multiprocessing as mp
+    from mirbft_amd import workloads as W
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=180) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g2 = W.c2_requests(n=8192, first=0)
+    assert res[0][1] + res[1][1] == g2.arena[: 8192 * 512].tobytes()
+    g5 = W.c5_storm(n=8192, first=0)
+    assert np.array_equal(np.concatenate([res[0][2], res[1][2]]), g5.len)
+    assert res[0][3] == res[1][3] == 2.0   # max over ranks
+
+
+def test_partition_matches_rank_slicing_balance():
+    from mirbft_amd.engine import partition_by_blocks, blocks_for_len
+    from mirbft_amd import workloads as W
+    w = W.c5_storm(n=1 << 14)
+    b = partition_by_blocks(w.len, 8)
+    blocks = np.array([blocks_for_len(int(x)) for x in w.len])
+    per = np.array([blocks[b[i]:b[i + 1]].sum() for i in range(8)])
+    assert per.sum() == blocks.sum()
+    assert per.max() - per.min() <= blocks.max()
