@@ -43,7 +43,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--config", default="c2", choices=["c2", "c3", "c3dd", "c4", "c5"])
+    p.add_argument("--config", default="c2",
+                   help="c2 (default) | c3 | c3dd (digest-of-digests form) | c4 | c5 | "
+                        "u:N:SIZE[:STRIDE] (experiment: N uniform messages via the uniform kernel; "
+                        "STRIDE 0 makes every lane hash the same cached message)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
     return p.parse_args()
@@ -64,6 +67,13 @@ def build_workload(cfg: str, rank: int, world: int):
         total = 1 << 23
         per = total // world            # c5 is quoted as 8M actions over the node
         return W.c5_storm(n=per, first=rank * per)
+    if cfg.startswith("u:"):
+        parts = cfg.split(":")
+        n, size = int(parts[1]), int(parts[2])
+        w = W.uniform_requests(n, size, W.SEED, rank * n, name=f"uniform experiment {n} x {size} B")
+        if len(parts) > 3:
+            w.uniform_stride = int(parts[3])
+        return w
     raise ValueError(cfg)
 
 
@@ -87,6 +97,19 @@ def cpu_baseline(w, seconds: float):
             "gbps": nbytes / el / 1e9,
             "sample": f"first {n} messages of the same workload, repeated for {el:.1f} s "
                       f"({done} digests), oracle/sha256_oracle.c single thread"}
+
+
+TRAFFIC_FILE = "profiles/r01_traffic.json"
+
+
+def measured_traffic(cfg: str):
+    """HBM bytes per launch from the committed PMC profile (tools/pmc_traffic.sh ->
+    tools/traffic_summary.py); None when this config was not profiled."""
+    try:
+        with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
+            return json.load(f)["configs"][cfg]["traffic_bytes_per_launch"]
+    except (OSError, KeyError, ValueError):
+        return None
 
 
 def verify_sample(w, d_out, k: int = 512) -> None:
@@ -130,6 +153,9 @@ def main():
 
         def step():
             eng.digest_of_digests_device(d_table, d_idx, d_begin, d_out, stream)
+    elif args.config.startswith("u:"):
+        def step():
+            eng.digest_uniform_device(d_arena, w.uniform_stride, int(w.len[0]), w.n, d_out, stream)
     else:
         d_order = None
         if not w.uniform_stride:
@@ -161,7 +187,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     eng.device_status()
-    verify_sample(w, d_out)
+    if not (args.config.startswith("u:") and w.uniform_stride != (int(w.len[0]) + 15) // 16 * 16):
+        verify_sample(w, d_out)
 
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -196,7 +223,9 @@ def main():
             "gbps_hashed": gbps,
             "kernel_ms_mean": kern_ms,
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS,
-                         "unit": "Tint32op/s", "frac": achieved / PEAK_VALU_TOPS, "traffic": None,
+                         "unit": "Tint32op/s", "frac": achieved / PEAK_VALU_TOPS,
+                         "traffic": measured_traffic(args.config),
+                         "traffic_source": TRAFFIC_FILE if measured_traffic(args.config) else None,
                          "ops_per_block": OPS_PER_BLOCK,
                          "algorithmic_bytes_per_launch": w.message_bytes + 32 * w.n + 16 * w.n},
         }

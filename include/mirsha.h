@@ -134,6 +134,8 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
 int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
                              const uint64_t* d_len, const uint32_t* d_order, uint64_t n,
                              uint8_t* d_out, void* stream);
+/* Uniform layout: message i = d_arena[i*stride : i*stride + msg_len] (stride a
+ * multiple of 16; messages may overlap, stride 0 hashes one message n times). */
 int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t stride,
                                uint64_t msg_len, uint64_t n, uint8_t* d_out, void* stream);
 int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const uint32_t* d_idx,

@@ -577,7 +577,6 @@ int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t s
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n == 0) return MSHA_OK;
   if (!d_arena || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
-  if (stride < msg_len) return fail(ctx, MSHA_ERR_INVALID_ARG, "stride < msg_len");
   if (stride % MSHA_DEVICE_ALIGN) return fail(ctx, MSHA_ERR_ALIGNMENT, "stride must be a multiple of 16");
   return guarded(ctx, [&] {
     hipStream_t st;
