@@ -188,6 +188,35 @@ class GPUHasher {
     return r;
   }
 
+  // Batched request intake: Client.Propose's per-call digest
+  // (clients.go:189-192) for a whole batch of proposals, one msha_digest_batch.
+  Result<std::vector<Bytes>> RequestDigests(const std::vector<Bytes>& requests) {
+    Result<std::vector<Bytes>> r;
+    size_t total = 0;
+    for (auto& q : requests) total += q.size();
+    Bytes arena(total + 1);
+    std::vector<uint64_t> off(requests.size() + 1), len(requests.size() + 1);
+    size_t pos = 0;
+    for (size_t i = 0; i < requests.size(); ++i) {
+      if (!requests[i].empty()) std::memcpy(arena.data() + pos, requests[i].data(), requests[i].size());
+      off[i] = pos;
+      len[i] = requests[i].size();
+      pos += requests[i].size();
+    }
+    Bytes out(32 * requests.size());
+    if (!requests.empty()) {
+      int rc = msha_digest_batch(ctx_, arena.data(), total, off.data(), len.data(), requests.size(),
+                                 out.data());
+      if (rc != MSHA_OK) {
+        r.err = "libmirsha error " + std::to_string(rc) + ": " + msha_last_error(ctx_);
+        return r;
+      }
+    }
+    for (size_t i = 0; i < requests.size(); ++i)
+      r.value.emplace_back(out.begin() + 32 * i, out.begin() + 32 * (i + 1));
+    return r;
+  }
+
   msha_ctx* ctx() { return ctx_; }
 
  private:

@@ -67,10 +67,11 @@ typedef struct {
   uint64_t messages;       /* digests produced */
   uint64_t message_bytes;  /* sum of unpadded message lengths */
   uint64_t blocks;         /* 64-byte compressions performed */
-  double pack_ms;          /* host packing into pinned staging */
-  double h2d_ms;           /* host -> device copies (wall, last call) */
-  double kernel_ms;        /* kernel time (HIP events, last call, max over devices) */
-  double d2h_ms;           /* device -> host copies (wall, last call) */
+  /* Last host-memory call, milliseconds of wall time: */
+  double plan_ms;          /* validation, sharding, size-class order, placement */
+  double pack_ms;          /* gathering payload bytes into pinned staging (threads) */
+  double device_ms;        /* first upload .. last kernel on the device (HIP events, max over GPUs) */
+  double total_ms;         /* whole call */
 } msha_stats;
 
 uint32_t msha_abi_version(void);

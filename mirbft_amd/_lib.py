@@ -35,10 +35,10 @@ class MshaStats(ctypes.Structure):
         ("messages", ctypes.c_uint64),
         ("message_bytes", ctypes.c_uint64),
         ("blocks", ctypes.c_uint64),
+        ("plan_ms", ctypes.c_double),
         ("pack_ms", ctypes.c_double),
-        ("h2d_ms", ctypes.c_double),
-        ("kernel_ms", ctypes.c_double),
-        ("d2h_ms", ctypes.c_double),
+        ("device_ms", ctypes.c_double),
+        ("total_ms", ctypes.c_double),
     ]
 
 

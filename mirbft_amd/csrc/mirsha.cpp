@@ -9,11 +9,14 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <exception>
 #include <new>
 #include <stdexcept>
 #include <string>
+#include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/mirsha.h"
@@ -90,22 +93,27 @@ struct PinBuf {
 struct Device {
   int id = 0;
   int cus = 256;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;       // kernels (and everything on single-stream paths)
+  hipStream_t copy_stream = nullptr;  // H2D of staged chunks, overlapping the kernels
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  hipEvent_t slot_free[2] = {nullptr, nullptr};  // staging slot s may be refilled
+  hipEvent_t chunk_in = nullptr;                 // last chunk's bytes are on the device
   DevBuf arena, off, len, order, out, err, idx, begin, table;
-  PinBuf h_arena, h_meta, h_out;
+  PinBuf h_arena, h_meta, h_out, slot[2];
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
   bool use_order = false;
   void release() {
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table}) b->release();
-    for (PinBuf* b : {&h_arena, &h_meta, &h_out}) b->release();
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
+    for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1]}) b->release();
+    for (hipEvent_t* e : {&ev0, &ev1, &slot_free[0], &slot_free[1], &chunk_in}) {
+      if (*e) (void)hipEventDestroy(*e);
+      *e = nullptr;
+    }
     if (stream) (void)hipStreamDestroy(stream);
-    ev0 = ev1 = nullptr;
-    stream = nullptr;
+    if (copy_stream) (void)hipStreamDestroy(copy_stream);
+    stream = copy_stream = nullptr;
   }
 };
 
@@ -188,66 +196,190 @@ int guarded(msha_ctx* ctx, F&& f) {
   }
 }
 
-// Shared tail of the host-memory entry points: `pack(dev)` fills dev.h_arena
-// and dev.h_meta (off then len, uint64 each, shard-local) for messages
-// [dev.lo, dev.hi); this function ships them, launches and collects.
-template <class Pack>
-void run_sharded(msha_ctx* ctx, uint64_t n, const uint64_t* msg_len_for_partition,
-                 uint8_t* out, Pack&& pack) {
+// Split [0, n) into nearly equal contiguous pieces and run f(lo, hi) on a few
+// host threads (gathering into pinned staging is host-bandwidth bound).
+template <class F>
+void parallel_ranges(uint64_t n, uint64_t bytes, F&& f) {
+  unsigned hw = std::thread::hardware_concurrency();
+  unsigned t = (unsigned)std::min<uint64_t>({(uint64_t)std::max(1u, std::min(8u, hw / 2)),
+                                             bytes / (4u << 20) + 1, n});
+  if (t <= 1) {
+    f(0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(t);
+  for (unsigned k = 0; k < t; ++k)
+    th.emplace_back([&, k] { f(n * k / t, n * (k + 1) / t); });
+  for (auto& x : th) x.join();
+}
+
+// Host-memory execution of one batch (the body of every host entry point):
+//   shard messages [0, n) over the context's GPUs by cumulative block count;
+//   per GPU, place its messages in descending-block order (a wave's lanes then
+//   run equal block counts) at 16-byte aligned offsets of the device arena,
+//   upload off/len(/order), and stream the payload in chunks through two pinned
+//   staging slots: host threads gather chunk c+1 while chunk c's H2D and kernel
+//   run (copy stream -> event -> kernel stream). Digests come back with one D2H
+//   per GPU at the end. gather(i, dst) copies message i's bytes to dst.
+constexpr uint64_t kChunkBytes = 32ull << 20;
+
+// uid (may be null): messages with equal uid[i] have identical bytes (aliases,
+// e.g. one EpochChange re-hashed N^2 times, epoch_target.go:486-505); their
+// payload is copied once per GPU.
+template <class Gather>
+void run_pipeline(msha_ctx* ctx, uint64_t n, const uint64_t* len, const uint64_t* uid, uint8_t* out,
+                  Gather&& gather) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   std::vector<uint64_t> bounds(k + 1);
-  if (k == 1) {
-    bounds[0] = 0;
-    bounds[1] = n;
-  } else {
-    partition(msg_len_for_partition, n, k, bounds.data());
-  }
-  double t0 = now_ms();
+  partition(len, n, k, bounds.data());
+  double t0 = now_ms(), gather_ms = 0;
+
+  struct Plan {
+    uint64_t m = 0;
+    bool ordered = false;
+    std::vector<uint32_t> perm;       // sorted lane -> shard-local message
+    std::vector<uint64_t> place;      // placement -> shard-local message whose bytes it holds
+    std::vector<uint64_t> ppos;       // placement -> device arena offset (size +1)
+    std::vector<uint64_t> lane_cut;   // chunk boundaries in sorted lanes
+    std::vector<uint64_t> place_cut;  // chunk boundaries in placements
+    size_t next = 0;                  // next chunk to issue
+  };
+  std::vector<Plan> plans(k);
+  // uid -> placement of its payload in the current shard (UINT64_MAX = none yet)
+  std::vector<uint64_t> placed(uid ? n : 0, UINT64_MAX);
+  std::vector<uint64_t> touched;  // uids placed in the current shard (reset per shard)
   for (uint32_t s = 0; s < k; ++s) {
     Device& d = ctx->devs[s];
+    Plan& P = plans[s];
     d.lo = bounds[s];
     d.hi = bounds[s + 1];
-    pack(d);
-  }
-  double t1 = now_ms();
-  // Enqueue H2D + kernel + D2H on every device, then join.
-  for (uint32_t s = 0; s < k; ++s) {
-    Device& d = ctx->devs[s];
-    const uint64_t m = d.hi - d.lo;
-    if (m == 0) continue;
-    HIPCHK(hipSetDevice(d.id));
-    d.arena.ensure(d.arena_bytes + msha::kArenaSlack);
-    d.off.ensure(8 * m);
-    d.len.ensure(8 * m);
-    d.out.ensure(32 * m);
-    d.err.ensure(4);
-    const uint64_t* h_off = d.h_meta.as<uint64_t>();
-    const uint64_t* h_len = h_off + m;
-    if (d.arena_bytes)
-      HIPCHK(hipMemcpyAsync(d.arena.p, d.h_arena.p, d.arena_bytes, hipMemcpyHostToDevice, d.stream));
-    HIPCHK(hipMemcpyAsync(d.off.p, h_off, 8 * m, hipMemcpyHostToDevice, d.stream));
-    HIPCHK(hipMemcpyAsync(d.len.p, h_len, 8 * m, hipMemcpyHostToDevice, d.stream));
-    const uint32_t* dorder = nullptr;
-    if (d.use_order) {
-      d.order.ensure(4 * m);
-      HIPCHK(hipMemcpyAsync(d.order.p, h_len + m, 4 * m, hipMemcpyHostToDevice, d.stream));
-      dorder = d.order.as<uint32_t>();
+    P.m = d.hi - d.lo;
+    if (P.m == 0) continue;
+    const uint64_t* L = len + d.lo;
+    P.ordered = !all_equal_blocks(L, P.m);
+    d.use_order = P.ordered;
+    P.perm.resize(P.m);
+    if (P.ordered) order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp);
+    else for (uint64_t i = 0; i < P.m; ++i) P.perm[i] = (uint32_t)i;
+    d.h_meta.ensure(16 * P.m + 4 * P.m);
+    uint64_t* h_off = d.h_meta.as<uint64_t>();
+    uint64_t* h_len = h_off + P.m;
+    // Place payloads in first-use order of the sorted lanes; aliased messages
+    // (same uid) share one placement, so every lane of chunk c reads bytes
+    // uploaded by the end of chunk c.
+    P.place.clear();
+    P.ppos.clear();
+    P.lane_cut.assign(1, 0);
+    P.place_cut.assign(1, 0);
+    uint64_t acc = 0, chunk_start = 0;
+    for (uint64_t q = 0; q < P.m; ++q) {
+      const uint32_t i = P.perm[q];
+      uint64_t at;
+      uint64_t* pl = uid ? &placed[uid[d.lo + i]] : nullptr;
+      if (pl && *pl != UINT64_MAX) {
+        at = P.ppos[*pl];
+      } else {
+        if (pl) {
+          *pl = P.place.size();
+          touched.push_back(uid[d.lo + i]);
+        }
+        P.place.push_back(i);
+        P.ppos.push_back(acc);
+        at = acc;
+        acc += round16(L[i]);
+      }
+      h_off[i] = at;
+      h_len[i] = L[i];
+      if (acc - chunk_start >= kChunkBytes && q + 1 < P.m) {
+        P.lane_cut.push_back(q + 1);
+        P.place_cut.push_back(P.place.size());
+        chunk_start = acc;
+      }
     }
+    for (uint64_t t : touched) placed[t] = UINT64_MAX;
+    touched.clear();
+    P.ppos.push_back(acc);
+    P.lane_cut.push_back(P.m);
+    P.place_cut.push_back(P.place.size());
+    d.arena_bytes = acc;
+    if (P.ordered) std::memcpy(h_len + P.m, P.perm.data(), 4 * P.m);
+    uint64_t slot_bytes = 0;
+    for (size_t c = 0; c + 1 < P.place_cut.size(); ++c)
+      slot_bytes = std::max(slot_bytes, P.ppos[P.place_cut[c + 1]] - P.ppos[P.place_cut[c]]);
+    d.slot[0].ensure(std::max<uint64_t>(slot_bytes, 16));
+    d.slot[1].ensure(std::max<uint64_t>(slot_bytes, 16));
+    HIPCHK(hipSetDevice(d.id));
+    d.arena.ensure(acc + msha::kArenaSlack);
+    d.off.ensure(8 * P.m);
+    d.len.ensure(8 * P.m);
+    d.out.ensure(32 * P.m);
+    d.err.ensure(4);
+    if (P.ordered) d.order.ensure(4 * P.m);
+    HIPCHK(hipMemcpyAsync(d.off.p, h_off, 8 * P.m, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(hipMemcpyAsync(d.len.p, h_len, 8 * P.m, hipMemcpyHostToDevice, d.stream));
+    if (P.ordered)
+      HIPCHK(hipMemcpyAsync(d.order.p, h_len + P.m, 4 * P.m, hipMemcpyHostToDevice, d.stream));
     HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
     HIPCHK(hipEventRecord(d.ev0, d.stream));
-    HIPCHK(msha::launch_digest_batch(d.arena.as<uint8_t>(), d.off.as<uint64_t>(),
-                                     d.len.as<uint64_t>(), dorder, m, d.out.as<uint8_t>(),
-                                     d.err.as<uint32_t>(), d.cus, d.stream));
+    HIPCHK(hipEventRecord(d.slot_free[0], d.copy_stream));
+    HIPCHK(hipEventRecord(d.slot_free[1], d.copy_stream));
+  }
+  const double t_plan = now_ms();
+  // Issue chunks round-robin over the GPUs so every copy engine stays busy.
+  for (bool more = true; more;) {
+    more = false;
+    for (uint32_t s = 0; s < k; ++s) {
+      Device& d = ctx->devs[s];
+      Plan& P = plans[s];
+      if (P.m == 0 || P.next + 1 >= P.lane_cut.size()) continue;
+      more = true;
+      const size_t c = P.next++;
+      const uint64_t q0 = P.lane_cut[c], q1 = P.lane_cut[c + 1];
+      const uint64_t u0 = P.place_cut[c], u1 = P.place_cut[c + 1];
+      const uint64_t b0 = P.ppos[u0], b1 = P.ppos[u1];
+      PinBuf& slot = d.slot[c & 1];
+      HIPCHK(hipSetDevice(d.id));
+      HIPCHK(hipEventSynchronize(d.slot_free[c & 1]));   // its previous H2D has drained
+      const double g0 = now_ms();
+      uint8_t* dst = slot.as<uint8_t>();
+      parallel_ranges(u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
+        for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.place[u], dst + (P.ppos[u] - b0));
+      });
+      gather_ms += now_ms() - g0;
+      if (b1 > b0)
+        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
+                              d.copy_stream));
+      HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
+      HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
+      HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
+      const uint64_t lanes = q1 - q0;
+      if (P.ordered) {
+        HIPCHK(msha::launch_digest_batch(d.arena.as<uint8_t>(), d.off.as<uint64_t>(),
+                                         d.len.as<uint64_t>(), d.order.as<uint32_t>() + q0, lanes,
+                                         d.out.as<uint8_t>(), d.err.as<uint32_t>(), d.cus, d.stream));
+      } else {  // identity placement: lane q hashes message q
+        HIPCHK(msha::launch_digest_batch(d.arena.as<uint8_t>(), d.off.as<uint64_t>() + q0,
+                                         d.len.as<uint64_t>() + q0, nullptr, lanes,
+                                         d.out.as<uint8_t>() + 32 * q0, d.err.as<uint32_t>(), d.cus,
+                                         d.stream));
+      }
+    }
+  }
+  for (uint32_t s = 0; s < k; ++s) {
+    Device& d = ctx->devs[s];
+    const uint64_t m = plans[s].m;
+    if (m == 0) continue;
+    HIPCHK(hipSetDevice(d.id));
     HIPCHK(hipEventRecord(d.ev1, d.stream));
     d.h_out.ensure(32 * m + 4);
     HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
-    HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost,
-                          d.stream));
+    HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
   }
   double kernel_ms = 0;
   for (uint32_t s = 0; s < k; ++s) {
     Device& d = ctx->devs[s];
-    const uint64_t m = d.hi - d.lo;
+    const uint64_t m = plans[s].m;
     if (m == 0) continue;
     HIPCHK(hipSetDevice(d.id));
     HIPCHK(hipStreamSynchronize(d.stream));
@@ -259,12 +391,11 @@ void run_sharded(msha_ctx* ctx, uint64_t n, const uint64_t* msg_len_for_partitio
     if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
     std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
   }
-  double t2 = now_ms();
   ctx->stats.calls++;
-  ctx->stats.pack_ms = t1 - t0;
-  ctx->stats.h2d_ms = t2 - t1;  // wall of enqueue..join (H2D + kernel + D2H)
-  ctx->stats.kernel_ms = kernel_ms;
-  ctx->stats.d2h_ms = 0;
+  ctx->stats.plan_ms = t_plan - t0;
+  ctx->stats.pack_ms = gather_ms;
+  ctx->stats.device_ms = kernel_ms;
+  ctx->stats.total_ms = now_ms() - t0;
 }
 
 }  // namespace
@@ -297,9 +428,16 @@ int msha_ctx_create(uint32_t device_mask, msha_ctx** out) {
   msha_ctx* ctx = new (std::nothrow) msha_ctx();
   if (!ctx) return MSHA_ERR_OUT_OF_MEMORY;
   int rc = guarded(ctx, [&] {
+    // MSHA_VIRTUAL_SHARDS=k (testing only): a one-device mask is split into k
+    // shards on that same GPU, each with its own streams and buffers, so the
+    // multi-GPU sharding path can be exercised on a one-GPU box.
+    int virt = 1;
+    if (const char* e = getenv("MSHA_VIRTUAL_SHARDS")) virt = std::max(1, std::min(8, atoi(e)));
+    if ((device_mask & (device_mask - 1)) != 0) virt = 1;
     for (int i = 0; i < 32; ++i) {
       if (!(device_mask & (1u << i))) continue;
       if (i >= count) throw MshaError(MSHA_ERR_NO_DEVICE, "device_mask names device " + std::to_string(i) + " but only " + std::to_string(count) + " visible");
+      for (int v = 0; v < virt; ++v) {
       Device d;
       d.id = i;
       HIPCHK(hipSetDevice(i));
@@ -307,9 +445,14 @@ int msha_ctx_create(uint32_t device_mask, msha_ctx** out) {
       HIPCHK(hipGetDeviceProperties(&prop, i));
       d.cus = prop.multiProcessorCount;
       HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+      HIPCHK(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
       HIPCHK(hipEventCreate(&d.ev0));
       HIPCHK(hipEventCreate(&d.ev1));
+      HIPCHK(hipEventCreateWithFlags(&d.slot_free[0], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&d.slot_free[1], hipEventDisableTiming));
+      HIPCHK(hipEventCreateWithFlags(&d.chunk_in, hipEventDisableTiming));
       ctx->devs.push_back(d);
+      }
     }
   });
   if (rc != MSHA_OK) {
@@ -374,51 +517,44 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
       return fail(ctx, MSHA_ERR_INVALID_ARG,
                   "message " + std::to_string(i) + " [off+len] outside arena");
   return guarded(ctx, [&] {
-    bool aligned = true;
-    for (uint64_t i = 0; i < n && aligned; ++i) aligned = (off[i] & 15) == 0;
-    run_sharded(ctx, n, len, out, [&](Device& d) {
-      const uint64_t m = d.hi - d.lo;
-      if (m == 0) { d.arena_bytes = 0; return; }
-      const bool ord = !all_equal_blocks(len + d.lo, m);
-      d.use_order = ord;
-      d.h_meta.ensure(16 * m + (ord ? 4 * m : 0));
-      uint64_t* h_off = d.h_meta.as<uint64_t>();
-      uint64_t* h_len = h_off + m;
-      if (aligned) {
-        // Payloads are already 16-byte aligned: ship the span the shard
-        // references once (aliased payloads are copied once per GPU).
-        uint64_t lo = UINT64_MAX, hi = 0;
-        for (uint64_t i = d.lo; i < d.hi; ++i) {
-          lo = std::min(lo, off[i]);
-          hi = std::max(hi, off[i] + len[i]);
-        }
-        lo &= ~uint64_t(15);
-        d.arena_bytes = round16(hi - lo);
-        d.h_arena.ensure(d.arena_bytes);
-        std::memcpy(d.h_arena.p, arena + lo, hi - lo);
-        for (uint64_t i = 0; i < m; ++i) {
-          h_off[i] = off[d.lo + i] - lo;
-          h_len[i] = len[d.lo + i];
-        }
-      } else {
-        uint64_t total = 0;
-        for (uint64_t i = d.lo; i < d.hi; ++i) total += round16(len[i]);
-        d.arena_bytes = total;
-        d.h_arena.ensure(total);
-        uint64_t pos = 0;
-        for (uint64_t i = 0; i < m; ++i) {
-          std::memcpy(d.h_arena.as<uint8_t>() + pos, arena + off[d.lo + i], len[d.lo + i]);
-          h_off[i] = pos;
-          h_len[i] = len[d.lo + i];
-          pos += round16(len[d.lo + i]);
+    // Overlapping payloads (sum of lengths > the span they cover) means aliases:
+    // give every message the index of the first message with the same (off, len).
+    uint64_t lo = UINT64_MAX, hi = 0, sum = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      lo = std::min(lo, off[i]);
+      hi = std::max(hi, off[i] + len[i]);
+      sum += len[i];
+    }
+    std::vector<uint64_t> uidv;
+    if (n > 1 && sum > hi - lo) {
+      // open-addressing table (linear probing) of first index + 1 per (off, len)
+      uint64_t cap = 1;
+      while (cap < 2 * n) cap <<= 1;
+      std::vector<uint64_t> table(cap, 0);
+      uidv.resize(n);
+      for (uint64_t i = 0; i < n; ++i) {
+        uint64_t hsh = (off[i] * 0x9E3779B97F4A7C15ull) ^ (len[i] * 0xC2B2AE3D27D4EB4Full);
+        hsh ^= hsh >> 29;
+        for (uint64_t p = hsh & (cap - 1);; p = (p + 1) & (cap - 1)) {
+          const uint64_t e = table[p];
+          if (e == 0) {
+            table[p] = i + 1;
+            uidv[i] = i;
+            break;
+          }
+          if (off[e - 1] == off[i] && len[e - 1] == len[i]) {
+            uidv[i] = e - 1;
+            break;
+          }
         }
       }
-      if (ord) order_by_blocks_desc(h_len, m, reinterpret_cast<uint32_t*>(h_len + m), ctx->sort_tmp);
-    });
-    uint64_t bytes = 0, blocks = 0;
-    for (uint64_t i = 0; i < n; ++i) { bytes += len[i]; blocks += blocks_for(len[i]); }
+    }
+    run_pipeline(ctx, n, len, uidv.empty() ? nullptr : uidv.data(), out,
+                 [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); });
+    uint64_t blocks = 0;
+    for (uint64_t i = 0; i < n; ++i) blocks += blocks_for(len[i]);
     ctx->stats.messages += n;
-    ctx->stats.message_bytes += bytes;
+    ctx->stats.message_bytes += sum;
     ctx->stats.blocks += blocks;
   });
 }
@@ -444,32 +580,11 @@ int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
     alen.assign(n_actions, 0);
     for (uint64_t i = 0; i < n_actions; ++i)
       for (uint64_t j = action_part_begin[i]; j < action_part_begin[i + 1]; ++j) alen[i] += part_len[j];
-    run_sharded(ctx, n_actions, alen.data(), out, [&](Device& d) {
-      const uint64_t m = d.hi - d.lo;
-      if (m == 0) { d.arena_bytes = 0; return; }
-      const bool ord = !all_equal_blocks(alen.data() + d.lo, m);
-      d.use_order = ord;
-      d.h_meta.ensure(16 * m + (ord ? 4 * m : 0));
-      uint64_t* h_off = d.h_meta.as<uint64_t>();
-      uint64_t* h_len = h_off + m;
-      uint64_t total = 0;
-      for (uint64_t i = d.lo; i < d.hi; ++i) total += round16(alen[i]);
-      d.arena_bytes = total;
-      d.h_arena.ensure(total);
-      uint8_t* dst = d.h_arena.as<uint8_t>();
-      uint64_t pos = 0;
-      for (uint64_t i = 0; i < m; ++i) {
-        const uint64_t a = d.lo + i;
-        h_off[i] = pos;
-        h_len[i] = alen[a];
-        uint64_t q = pos;
-        for (uint64_t j = action_part_begin[a]; j < action_part_begin[a + 1]; ++j) {
-          std::memcpy(dst + q, arena + part_off[j], part_len[j]);
-          q += part_len[j];
-        }
-        pos += round16(alen[a]);
+    run_pipeline(ctx, n_actions, alen.data(), nullptr, out, [&](uint64_t a, uint8_t* dst) {
+      for (uint64_t j = action_part_begin[a]; j < action_part_begin[a + 1]; ++j) {
+        std::memcpy(dst, arena + part_off[j], part_len[j]);
+        dst += part_len[j];
       }
-      if (ord) order_by_blocks_desc(h_len, m, reinterpret_cast<uint32_t*>(h_len + m), ctx->sort_tmp);
     });
     uint64_t bytes = 0, blocks = 0;
     for (uint64_t i = 0; i < n_actions; ++i) { bytes += alen[i]; blocks += blocks_for(alen[i]); }
@@ -543,8 +658,10 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
     ctx->stats.messages += n;
     ctx->stats.message_bytes += 32 * n_idx;
     ctx->stats.blocks += blocks;
-    ctx->stats.kernel_ms = kernel_ms;
-    ctx->stats.h2d_ms = now_ms() - t0;
+    ctx->stats.plan_ms = 0;
+    ctx->stats.pack_ms = 0;
+    ctx->stats.device_ms = kernel_ms;
+    ctx->stats.total_ms = now_ms() - t0;
   });
 }
 

@@ -26,6 +26,8 @@ from __future__ import annotations
 from dataclasses import dataclass, field
 from typing import Any, Iterator, List, Optional, Sequence, Union
 
+import numpy as np
+
 from .encoding import EpochChange, RequestAck
 from .engine import Engine
 
@@ -182,6 +184,21 @@ class GPUHasher:
 
     def hash_batch(self, actions: Sequence[Sequence[bytes]]) -> List[bytes]:
         return self.engine.hash_actions(actions)
+
+    def request_digests(self, requests: Sequence[bytes]) -> List[bytes]:
+        """Batched request intake: the digest that
+        Client.Propose computes per call (clients.go:189-192, ``h.Write(data);
+        h.Sum(nil)``) for a whole batch of proposals, in one GPU call
+        (msha_digest_batch over a packed arena)."""
+        if not requests:
+            return []
+        lens = np.fromiter((len(r) for r in requests), dtype=np.uint64, count=len(requests))
+        offs = np.zeros(len(requests), dtype=np.uint64)
+        if len(requests) > 1:
+            offs[1:] = np.cumsum(lens)[:-1]
+        arena = np.frombuffer(b"".join(bytes(r) for r in requests), dtype=np.uint8)
+        out = self.engine.digest_batch(arena, offs, lens)
+        return [bytes(r) for r in out]
 
 
 def ProcessHashActions(hasher: GPUHasher, actions: ActionList) -> EventList:

@@ -99,6 +99,14 @@ int main() {
     Bytes s = h.Sum(pre);
     EXPECT(s.size() == 35 && Bytes(s.begin(), s.begin() + 3) == pre, "Sum(b) appends");
   }
+  {  // Describe("RequestDigests") It("matches Client.Propose's per-request digest")
+    std::vector<Bytes> reqs;
+    for (int i = 0; i < 300; ++i) reqs.push_back(Bytes(i * 7 % 600, (uint8_t)i));
+    auto r = hasher.RequestDigests(reqs);
+    EXPECT(r.ok() && r.value.size() == reqs.size(), "one digest per request");
+    for (size_t i = 0; i < reqs.size() && i < r.value.size(); ++i)
+      EXPECT(r.value[i] == oracle({reqs[i]}), "request digest == oracle");
+  }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;

@@ -305,3 +305,37 @@ def test_c5_device_ordered(engine):
     engine.digest_batch_device(d_arena, d_off, d_len, out, order=d_order)
     engine.device_status()
     assert np.array_equal(out.cpu().numpy(), oracle.digest_batch(w.arena, w.off, w.len))
+
+
+@pytest.mark.parametrize("shards", [2, 3])
+def test_host_path_sharded(shards, monkeypatch):
+    """The multi-GPU host path (partition by blocks, per-shard placement, alias
+    dedup reset per shard, per-shard order) on virtual shards of one GPU."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", str(shards))
+    with Engine(1) as e:
+        w = W.c5_storm(1 << 15)                      # aliased EpochChange pool + mixed sizes
+        assert np.array_equal(e.digest_batch(w.arena, w.off, w.len),
+                              oracle.digest_batch(w.arena, w.off, w.len))
+        rng = np.random.default_rng(shards)
+        actions = [[rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+                    for _ in range(int(rng.integers(0, 4)))] for _ in range(5000)]
+        assert e.hash_actions(actions) == oracle.process_hash_actions(actions)
+        st = e.stats()
+        assert st["calls"] == 2 and st["messages"] == w.n + len(actions)
+
+
+def test_host_path_chunked_large_batch(engine):
+    """A batch spanning many 32 MiB staging chunks (c2 at full size) through the host API."""
+    w = W.c2_requests()
+    got = engine.digest_batch(w.arena, w.off, w.len)
+    assert np.array_equal(got, oracle.digest_batch(w.arena, w.off, w.len))
+
+
+def test_request_digests_batched_intake(engine):
+    """8f-1: Client.Propose's digest (clients.go:189-192) for a batch of proposals in one call."""
+    from mirbft_amd.encoding import recorder_request_bytes
+    reqs = [recorder_request_bytes(c, r) for c in range(4) for r in range(200)] + [b"", b"x" * 512]
+    got = GPUHasher(engine).request_digests(reqs)
+    assert got == [hashlib.sha256(r).digest() for r in reqs]
+    assert GPUHasher(engine).request_digests([]) == []
