@@ -17,17 +17,26 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <type_traits>
+
 #include "sha256_device.hpp"
 #include "kernels.hpp"
 
 namespace msha {
 
+// Mode bit 4 (kNT): payload loads carry the nontemporal (streaming) cache
+// policy -- every payload byte is read exactly once.
+constexpr int kNT = 4;
+
+template <int MODE = 0>
 __device__ __forceinline__ void load_block16(const uint8_t* p, uint32_t (&raw)[16]) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const u32x4* q = reinterpret_cast<const u32x4*>(p);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    u32x4 v = q[i];
+    u32x4 v;
+    if (MODE & kNT) v = __builtin_nontemporal_load(q + i);
+    else v = q[i];
     raw[4 * i + 0] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
   }
 }
@@ -73,24 +82,25 @@ __device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uin
   const uint32_t nvalu = nblocks - (upad ? 1 : 0);
   uint32_t raw[16];
   uint32_t w[16];
-  if (MODE == kPrefetch) load_block16(p, raw);
+  constexpr int LM = MODE & 3;  // load mode; MODE & kNT selects the cache policy
+  if (LM == kPrefetch) load_block16<MODE>(p, raw);
   for (uint32_t b = 0; b < nvalu; ++b) {
     const uint8_t* pb = p + 64 * (uint64_t)b;
-    if (MODE == kSingle && b <= nfull) load_block16(pb, raw);
-    if (MODE == kPair && b == nfull && !(b & 1)) load_block16(pb, raw);
+    if (LM == kSingle && b <= nfull) load_block16<MODE>(pb, raw);
+    if (LM == kPair && b == nfull && !(b & 1)) load_block16<MODE>(pb, raw);
     if (b < nfull) {
-      if (MODE == kPair) {
+      if (LM == kPair) {
         if (!(b & 1)) {
           uint32_t t[16];
-          load_block16(pb, t);
-          load_block16(pb + 64, raw);  // block b+1, or the tail block's bytes (slack-safe)
+          load_block16<MODE>(pb, t);
+          load_block16<MODE>(pb + 64, raw);  // block b+1, or the tail block's bytes (slack-safe)
           to_words(t, w);
         } else {
           to_words(raw, w);
         }
       } else {
         to_words(raw, w);
-        if (MODE == kPrefetch) load_block16(pb + 64, raw);
+        if (LM == kPrefetch) load_block16<MODE>(pb + 64, raw);
       }
     } else if (b == nfull) {
       // Launder r so the 16 per-dword tail masks are built here, once, and
@@ -200,34 +210,42 @@ __global__ __launch_bounds__(256, 8) void k_digest_of_digests(const uint8_t* __r
 static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 // Fewer than ~3 waves per SIMD cannot hide HBM latency by occupancy: use the
-// register-prefetching variant then; otherwise pair loads. MSHA_LOAD_MODE
-// (0/1/2) overrides, for A/B measurements.
+// register-prefetching variant then; otherwise pair loads. For A/B
+// measurements MSHA_LOAD_MODE (0/1/2) forces the load mode and MSHA_NT=1 the
+// nontemporal payload loads.
+static inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 static inline int pick_mode(uint64_t n, int cus) {
-  static const int forced = [] {
-    const char* e = getenv("MSHA_LOAD_MODE");
-    return e ? atoi(e) : -1;
-  }();
-  if (forced >= 0 && forced <= 2) return forced;
-  return n < (uint64_t)cus * 4 * 64 * 3 ? kPrefetch : kPair;
+  static const int forced = env_int("MSHA_LOAD_MODE", -1);
+  static const int nt = env_int("MSHA_NT", 0) ? kNT : 0;
+  const int lm = (forced >= 0 && forced <= 2) ? forced
+                 : (n < (uint64_t)cus * 4 * 64 * 3 ? kPrefetch : kPair);
+  return lm | nt;
+}
+
+// Calls f(std::integral_constant<int, MODE>) for the runtime mode.
+template <class F>
+static inline void with_mode(int mode, F&& f) {
+  switch (mode) {
+    case kSingle: f(std::integral_constant<int, kSingle>()); break;
+    case kPrefetch: f(std::integral_constant<int, kPrefetch>()); break;
+    case kPair: f(std::integral_constant<int, kPair>()); break;
+    case kSingle | kNT: f(std::integral_constant<int, kSingle | kNT>()); break;
+    case kPrefetch | kNT: f(std::integral_constant<int, kPrefetch | kNT>()); break;
+    default: f(std::integral_constant<int, kPair | kNT>()); break;
+  }
 }
 
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
                                const uint32_t* order, uint64_t n, uint8_t* out, uint32_t* err,
                                int cus, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  switch (pick_mode(n, cus)) {
-    case kSingle:
-      hipLaunchKernelGGL(k_digest_batch<kSingle>, dim3(grid_for(n)), dim3(256), 0, st, arena, off,
-                         len, order, n, out, err);
-      break;
-    case kPrefetch:
-      hipLaunchKernelGGL(k_digest_batch<kPrefetch>, dim3(grid_for(n)), dim3(256), 0, st, arena, off,
-                         len, order, n, out, err);
-      break;
-    default:
-      hipLaunchKernelGGL(k_digest_batch<kPair>, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
-                         order, n, out, err);
-  }
+  with_mode(pick_mode(n, cus), [&](auto m) {
+    hipLaunchKernelGGL(k_digest_batch<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
+                       arena, off, len, order, n, out, err);
+  });
   return hipGetLastError();
 }
 
@@ -235,19 +253,10 @@ hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st) {
   if (n == 0) return hipSuccess;
-  switch (pick_mode(n, cus)) {
-    case kSingle:
-      hipLaunchKernelGGL(k_digest_uniform<kSingle>, dim3(grid_for(n)), dim3(256), 0, st, arena,
-                         stride, msg_len, n, out, err);
-      break;
-    case kPrefetch:
-      hipLaunchKernelGGL(k_digest_uniform<kPrefetch>, dim3(grid_for(n)), dim3(256), 0, st, arena,
-                         stride, msg_len, n, out, err);
-      break;
-    default:
-      hipLaunchKernelGGL(k_digest_uniform<kPair>, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
-                         msg_len, n, out, err);
-  }
+  with_mode(pick_mode(n, cus), [&](auto m) {
+    hipLaunchKernelGGL(k_digest_uniform<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
+                       arena, stride, msg_len, n, out, err);
+  });
   return hipGetLastError();
 }
 
