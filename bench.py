@@ -259,6 +259,11 @@ def main():
                          "traffic": measured_traffic(args.config),
                          "traffic_source": TRAFFIC_FILE if measured_traffic(args.config) else None,
                          "ops_per_block": OPS_PER_BLOCK,
+                         "note": "peak = full-rate int32 VALU (VOP2/v_bitop3, 2 cycles per wave64 "
+                                 "instr at 2.4 GHz); SHA-256's mix is 64% half-rate ops (v_alignbit, "
+                                 "v_add3) and costs ~4 SIMD cycles per instruction on gfx950, so the "
+                                 "ISA-mix ceiling measured on a register-resident loop is ~0.50 of "
+                                 "this peak (DESIGN.md, profiles/r01_valu_microbench*)",
                          "algorithmic_bytes_per_launch": w.message_bytes + 32 * w.n + 16 * w.n},
         }
         if not args.no_cpu_baseline and world == 1:

@@ -339,3 +339,11 @@ def test_request_digests_batched_intake(engine):
     got = GPUHasher(engine).request_digests(reqs)
     assert got == [hashlib.sha256(r).digest() for r in reqs]
     assert GPUHasher(engine).request_digests([]) == []
+
+
+def test_missing_device_in_mask_is_an_error():
+    from mirbft_amd import Engine, device_count
+    n = device_count()
+    with pytest.raises(MshaError) as ei:
+        Engine(1 << n)          # one past the last visible device
+    assert ei.value.code == L.MSHA_ERR_NO_DEVICE
