@@ -8,7 +8,8 @@
 //
 // Data layout in HBM (see DESIGN.md "Data layout"):
 //   arena  : message bytes, each message 16-byte aligned (the host packer
-//            guarantees this; other alignments take a slower correct path)
+//            guarantees this; a misaligned device-API message is flagged and
+//            its digest zeroed, never computed wrongly), 64 B slack at the end
 //   off/len: uint64 per message (several messages may alias one payload)
 //   order  : optional uint32 permutation (size-class binning: lanes of a wave
 //            get messages of equal block count so no lane idles)
