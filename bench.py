@@ -44,7 +44,8 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="c2",
-                   help="c2 (default) | c3 | c3dd (digest-of-digests form) | c4 | c5 | "
+                   help="c2 (default) | c3 | c3dd (digest-of-digests form) | c4 | c5 | ub:N:SIZE (experiment: "
+                        "N uniform messages via the batch kernel) | "
                         "u:N:SIZE[:STRIDE] (experiment: N uniform messages via the uniform kernel; "
                         "STRIDE 0 makes every lane hash the same cached message)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -52,6 +53,8 @@ def parse():
     p.add_argument("--e2e", action="store_true",
                    help="instead: time the HOST entry point (pack + PCIe H2D + kernel + D2H) on the "
                         "same workload; prints an end-to-end line (never the headline value)")
+    p.add_argument("--policy", default="auto", choices=["auto", "lane", "coop"],
+                   help="batch-kernel policy (msha_set_kernel_policy); digests are identical")
     p.add_argument("--share-device", action="store_true",
                    help="rehearsal only: every rank uses GPU 0 (multi-rank path on a 1-GPU box)")
     return p.parse_args()
@@ -72,6 +75,9 @@ def build_workload(cfg: str, rank: int, world: int):
         total = 1 << 23
         per = total // world            # c5 is quoted as 8M actions over the node
         return W.c5_storm(n=per, first=rank * per)
+    if cfg.startswith("ub:"):        # uniform sizes through the batch (off/len) kernel
+        n, size = (int(x) for x in cfg.split(":")[1:3])
+        return W.uniform_requests(n, size, W.SEED, rank * n, name=f"batch-kernel experiment {n} x {size} B")
     if cfg.startswith("u:"):
         parts = cfg.split(":")
         n, size = int(parts[1]), int(parts[2])
@@ -129,11 +135,12 @@ def verify_sample(w, d_out, k: int = 512) -> None:
 
 def run_e2e(args, eng, w, world):
     """End-to-end host path: numpy arena in pageable host memory -> digests in host memory."""
+    out = np.empty((w.n, 32), dtype=np.uint8)   # a node reuses its result buffer
     for _ in range(max(1, args.warmup)):
-        out = eng.digest_batch(w.arena, w.off, w.len)
+        eng.digest_batch(w.arena, w.off, w.len, out=out)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        out = eng.digest_batch(w.arena, w.off, w.len)
+        eng.digest_batch(w.arena, w.off, w.len, out=out)
     el = time.perf_counter() - t0
     st = eng.stats()
     from oracle import oracle
@@ -167,6 +174,7 @@ def main():
 
     from mirbft_amd import Engine
     eng = Engine(1 << local)
+    eng.set_kernel_policy(args.policy)
     w = build_workload(args.config, rank, world)
     if args.e2e:
         return run_e2e(args, eng, w, world)
@@ -214,9 +222,12 @@ def main():
         step()
         e1.record(stream)
     torch.cuda.synchronize(dev)
+    # This rank's span ends when its GPU has drained; the closing barrier (and
+    # the max over ranks below) then gives the job's makespan without charging
+    # the control-plane barrier's own latency to the hash path.
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     eng.device_status()
     if not (args.config.startswith("u:") and w.uniform_stride != (int(w.len[0]) + 15) // 16 * 16):

@@ -68,7 +68,7 @@ typedef struct {
   uint64_t message_bytes;  /* sum of unpadded message lengths */
   uint64_t blocks;         /* 64-byte compressions performed */
   /* Last host-memory call, milliseconds of wall time: */
-  double plan_ms;          /* validation, sharding, size-class order, placement */
+  double plan_ms;          /* validation, alias detection, sharding, size-class order, placement */
   double pack_ms;          /* gathering payload bytes into pinned staging (threads) */
   double device_ms;        /* first upload .. last kernel on the device (HIP events, max over GPUs) */
   double total_ms;         /* whole call */
@@ -145,6 +145,21 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
 /* Synchronizes the context's first device and reports (then clears) any
  * device-side error flag raised by *_device calls: MSHA_OK or MSHA_ERR_ALIGNMENT. */
 int msha_device_status(msha_ctx* ctx);
+
+/*
+ * Kernel policy for one-part messages (msha_digest_batch, msha_hash_actions,
+ * msha_digest_batch_device). Results are identical under every policy.
+ *  MSHA_KERNEL_AUTO  (default) one lane per message when a launch has enough
+ *                    messages to give every SIMD a wavefront; otherwise
+ *                    cooperative chaining
+ *  MSHA_KERNEL_LANE  always one wavefront lane per message
+ *  MSHA_KERNEL_COOP  always cooperative chaining: per 64 messages a producer
+ *                    wavefront expands the message schedules into LDS while a
+ *                    consumer wavefront runs only the rounds (lower latency per
+ *                    message; for few, large messages)
+ */
+enum { MSHA_KERNEL_AUTO = 0, MSHA_KERNEL_LANE = 1, MSHA_KERNEL_COOP = 2 };
+int msha_set_kernel_policy(msha_ctx* ctx, int policy);
 
 /* Pinned host memory for callers that want zero-copy staging. */
 int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p);

@@ -22,6 +22,9 @@ MSHA_ERR_OUT_OF_MEMORY = 4
 MSHA_ERR_ALIGNMENT = 5
 MSHA_DEVICE_ARENA_SLACK = 64
 MSHA_DEVICE_ALIGN = 16
+MSHA_KERNEL_AUTO = 0
+MSHA_KERNEL_LANE = 1
+MSHA_KERNEL_COOP = 2
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -65,6 +68,7 @@ SIGNATURES = {
                                                      ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                                      ctypes.c_void_p]),
     "msha_device_status": (ctypes.c_int, [_ctxp]),
+    "msha_set_kernel_policy": (ctypes.c_int, [_ctxp, ctypes.c_int]),
     "msha_pinned_alloc": (ctypes.c_int, [_ctxp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "msha_pinned_free": (ctypes.c_int, [_ctxp, ctypes.c_void_p]),
     "msha_blocks_for_len": (ctypes.c_uint64, [ctypes.c_uint64]),

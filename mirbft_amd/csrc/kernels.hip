@@ -170,6 +170,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
                                                       const uint64_t* __restrict__ off,
                                                       const uint64_t* __restrict__ len,
                                                       const uint32_t* __restrict__ order,
+                                                      const uint32_t* __restrict__ out_idx,
                                                       uint64_t n, uint8_t* __restrict__ out,
                                                       uint32_t* __restrict__ err) {
   // kLds: one 4 KiB LDS slice per wave (16 KiB per 256-thread workgroup,
@@ -177,10 +178,152 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
   __shared__ __attribute__((aligned(16))) uint8_t lds[(MODE & 3) == kLds ? 4 * 4096 : 16];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t m = order ? (uint64_t)order[i] : i;
+  const uint64_t m = order ? (uint64_t)order[i] : i;      // metadata index
+  const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;  // digest slot
   const uint8_t* p = arena + off[m];
-  if (check_aligned(p, out + 32 * m, err))
-    hash_message<MODE>(p, len[m], out + 32 * m, lds + 4096 * (threadIdx.x / 64));
+  if (check_aligned(p, out + 32 * o, err))
+    hash_message<MODE>(p, len[m], out + 32 * o, lds + 4096 * (threadIdx.x / 64));
+}
+
+// ---------------------------------------------------------------------------
+// Cooperative chaining (few, large messages). A message's 64 rounds per block
+// are a serial chain, but its message schedule is not part of that chain: it
+// depends only on the block's bytes. A workgroup of two waves serves 64
+// messages: wave 1 (producer) lane l loads block b+1 of message l, expands its
+// schedule and writes K[t]+W[t] for t = 0..63 into an LDS slot, while wave 0
+// (consumer) lane l runs the 64 rounds of block b from the other slot. The
+// chain then costs 14 VALU instructions per round plus 16 ds_read_b128 per
+// block instead of 1,400 instructions per block: ~1.5x lower latency per
+// message, for batches too small to fill the chip with one lane per message.
+// ---------------------------------------------------------------------------
+// kw slot layout: [quad t/4][lane] x 16 B (K[t..t+3] + W[t..t+3]); every
+// ds_write_b128 / ds_read_b128 of a wave covers 1 KiB contiguously.
+constexpr int kCoopSlotQuads = 16;
+
+#define MSHA_CROUND(a, b, c, d, e, f, g, h, kw)          \
+  {                                                       \
+    uint32_t t1 = h + (kw) + Sig1(e) + ch(e, f, g);       \
+    d += t1;                                              \
+    h = t1 + Sig0(a) + maj(a, b, c);                      \
+  }
+#define MSHA_C8(q)                                                     \
+  {                                                                    \
+    const uint4 v0 = kv[q], v1 = kv[(q) + 1];                          \
+    MSHA_CROUND(a, b, c, d, e, f, g, h, v0.x)                          \
+    MSHA_CROUND(h, a, b, c, d, e, f, g, v0.y)                          \
+    MSHA_CROUND(g, h, a, b, c, d, e, f, v0.z)                          \
+    MSHA_CROUND(f, g, h, a, b, c, d, e, v0.w)                          \
+    MSHA_CROUND(e, f, g, h, a, b, c, d, v1.x)                          \
+    MSHA_CROUND(d, e, f, g, h, a, b, c, v1.y)                          \
+    MSHA_CROUND(c, d, e, f, g, h, a, b, v1.z)                          \
+    MSHA_CROUND(b, c, d, e, f, g, h, a, v1.w)                          \
+  }
+
+// Consumer: the 64 rounds of one block from a K+W slot (lane's column).
+__device__ __forceinline__ void compress_kw(State& s, const uint4* __restrict__ slot) {
+  // All 16 reads issued up front (64 VGPRs; this kernel runs at low
+  // occupancy): one LDS latency per block instead of one per quad.
+  uint4 kv[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) kv[q] = slot[q * 64];
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+  uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+  MSHA_C8(0) MSHA_C8(2) MSHA_C8(4) MSHA_C8(6) MSHA_C8(8) MSHA_C8(10) MSHA_C8(12) MSHA_C8(14)
+  s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+  s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+#undef MSHA_C8
+#undef MSHA_CROUND
+
+// Producer: expand block words w into K[t]+W[t], t = 0..63, written to the slot.
+__device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], uint4* __restrict__ slot) {
+  constexpr uint32_t K[64] = {MSHA_K_TABLE};
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    uint32_t x[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = 4 * q + j;
+      if (t >= 16) MSHA_SCHED(w, t);
+      x[j] = w[t & 15] + K[t];
+    }
+    slot[q * 64] = make_uint4(x[0], x[1], x[2], x[3]);
+  }
+}
+
+// Workgroup = 4 waves serving 128 messages: waves 0/1 consume (rounds) for
+// message groups 0/1, waves 2/3 produce (schedules) for the same groups. A
+// workgroup's waves take SIMDs in the cyclic order 0->2->1->3, so each wave
+// gets a SIMD of its own; the launch reserves enough LDS (kCoopLdsBytes) that
+// a CU holds ONE such workgroup, so a consumer never shares its SIMD with
+// another consumer (that would forfeit the latency gain).
+constexpr unsigned kCoopMsgsPerWg = 128;
+constexpr size_t kCoopDynLds = 40 * 1024;  // + 64 KiB static = 104 KiB > 160/2 KiB
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__ arena,
+                                                     const uint64_t* __restrict__ off,
+                                                     const uint64_t* __restrict__ len,
+                                                     const uint32_t* __restrict__ order,
+                                                     const uint32_t* __restrict__ out_idx,
+                                                     uint64_t n, uint8_t* __restrict__ out,
+                                                     uint32_t* __restrict__ err) {
+  __shared__ uint4 kw[2][2][kCoopSlotQuads * 64];  // [slot][group][quad][lane]: 64 KiB
+  __shared__ uint32_t s_nb;
+  const unsigned lane = threadIdx.x & 63;
+  const unsigned wave = threadIdx.x >> 6;
+  const bool producer = wave >= 2;
+  const unsigned group = wave & 1;
+  const uint64_t i = (uint64_t)blockIdx.x * kCoopMsgsPerWg + group * 64 + lane;
+  bool active = i < n;
+  const uint64_t m = active ? (order ? (uint64_t)order[i] : i) : 0;  // metadata index
+  const uint64_t o = active ? (out_idx ? (uint64_t)out_idx[i] : m) : 0;  // digest slot
+  const uint8_t* p = arena;
+  uint64_t L = 0;
+  if (active) {
+    p = arena + off[m];
+    L = len[m];
+    if (reinterpret_cast<uintptr_t>(p) & 15) {  // flagged and zeroed by the consumer only
+      active = false;
+      L = 0;
+      if (!producer) check_aligned(p, out + 32 * o, err);
+    }
+  }
+  const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
+  const uint32_t nb = nfull + (r < 56 ? 1 : 2);
+  if (threadIdx.x == 0) s_nb = 0;
+  __syncthreads();
+  if (!producer && active) atomicMax(&s_nb, nb);
+  __syncthreads();
+  const uint32_t NB = s_nb;  // blocks of the workgroup's longest message
+  // One barrier per block in every wave: after barrier k the producers have
+  // filled slot k&1 and the consumers are done with slot (k-1)&1.
+  if (producer) {
+    uint32_t raw[16], w[16];
+    if (active) load_block16<MODE>(p, raw);
+    for (uint32_t b = 0; b < NB; ++b) {
+      if (b < nfull) {
+        to_words(raw, w);
+      } else if (b == nfull) {
+        uint32_t rr = r;
+        asm volatile("" : "+v"(rr));
+        build_tail(raw, rr, L, w);
+      } else {
+        length_block(L, w);
+      }
+      if (active && b + 1 <= nfull) load_block16<MODE>(p + 64 * (uint64_t)(b + 1), raw);  // prefetch
+      schedule_kw(w, &kw[b & 1][group][lane]);
+      __syncthreads();
+    }
+  } else {
+    State s;
+    state_init(s);
+    for (uint32_t b = 0; b < NB; ++b) {
+      __syncthreads();
+      compress_kw(s, &kw[b & 1][group][lane]);
+      if (active && b + 1 == nb) store_digest(s, out + 32 * o);
+    }
+  }
 }
 
 // Uniform layout: message i is arena[i*stride : i*stride + msg_len].
@@ -266,6 +409,17 @@ static inline int pick_mode(uint64_t n, int cus) {
   return lm | nt;
 }
 
+// Cooperative chaining (AUTO) when every workgroup of the launch gets a CU of
+// its own (n <= 128 per CU): below that one lane per message leaves at least
+// half the SIMDs idle, and each consumer's chain runs 905 instead of ~1,400
+// instructions per block (profiles/r01_ab_coop: 1.2-1.5x). Above it a second
+// round of workgroups would cost more than the lane kernel's single round.
+bool uses_coop(uint64_t n, int cus, int policy) {
+  if (policy == 2) return true;   // MSHA_KERNEL_COOP
+  if (policy == 1) return false;  // MSHA_KERNEL_LANE
+  return n <= (uint64_t)cus * kCoopMsgsPerWg;
+}
+
 // Calls f(std::integral_constant<int, MODE>) for the runtime mode.
 template <class F>
 static inline void with_mode(int mode, F&& f) {
@@ -281,12 +435,20 @@ static inline void with_mode(int mode, F&& f) {
 }
 
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
-                               const uint32_t* order, uint64_t n, uint8_t* out, uint32_t* err,
-                               int cus, hipStream_t st) {
+                               const uint32_t* order, const uint32_t* out_idx, uint64_t n,
+                               uint8_t* out, uint32_t* err, int cus, int policy, hipStream_t st) {
   if (n == 0) return hipSuccess;
+  if (uses_coop(n, cus, policy)) {
+    const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
+    if (env_int("MSHA_NT", 0))
+      hipLaunchKernelGGL(k_digest_coop<kNT>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len, order, out_idx, n, out, err);
+    else
+      hipLaunchKernelGGL(k_digest_coop<0>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len, order, out_idx, n, out, err);
+    return hipGetLastError();
+  }
   with_mode(pick_mode(n, cus), [&](auto m) {
     hipLaunchKernelGGL(k_digest_batch<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
-                       arena, off, len, order, n, out, err);
+                       arena, off, len, order, out_idx, n, out, err);
   });
   return hipGetLastError();
 }

@@ -9,9 +9,15 @@ namespace msha {
 // kernels read a message's final block as one whole 64-byte block.
 constexpr uint64_t kArenaSlack = 64;
 
+// Lane i hashes message m = order ? order[i] : i (arena + off[m], len[m]) into
+// digest slot o = out_idx ? out_idx[i] : m (out + 32 o). The device API passes
+// order (message-indexed metadata); the host pipeline passes lane-indexed
+// metadata and out_idx. policy: MSHA_KERNEL_AUTO / _LANE / _COOP (mirsha.h).
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
-                               const uint32_t* order, uint64_t n, uint8_t* out, uint32_t* err,
-                               int cus, hipStream_t st);
+                               const uint32_t* order, const uint32_t* out_idx, uint64_t n,
+                               uint8_t* out, uint32_t* err, int cus, int policy, hipStream_t st);
+// Does launch_digest_batch use cooperative chaining for an n-message launch?
+bool uses_coop(uint64_t n, int cus, int policy);
 hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st);

@@ -117,26 +117,45 @@ struct Device {
   }
 };
 
-// Descending-block-count permutation (LSD radix on 32-bit keys) so every
-// wavefront gets messages of equal length and no lane idles.
-void order_by_blocks_desc(const uint64_t* len, uint64_t n, uint32_t* order, std::vector<uint32_t>& tmp) {
-  std::vector<uint32_t> key(n);
-  for (uint64_t i = 0; i < n; ++i) {
-    uint64_t b = blocks_for(len[i]);
-    key[i] = 0xffffffffu - (uint32_t)std::min<uint64_t>(b, 0xffffffffu);
+// Descending-block-count permutation so every wavefront gets messages of equal
+// length and no lane idles. Stable. Batches rarely hold more than a few dozen
+// distinct block counts, so a one-pass counting sort over [0, max blocks]
+// (scattered writes into that many sequential streams) is the common path;
+// messages beyond 2^20 blocks (64 MiB) fall back to a two-pass LSD radix.
+// rep (may be null): only messages with rep[i] == i are ordered (aliases of
+// another message get no lane). Returns the number of entries written.
+uint64_t order_by_blocks_desc(const uint64_t* len, uint64_t n, uint32_t* order,
+                              std::vector<uint32_t>& tmp, const uint32_t* rep = nullptr) {
+  auto keep = [&](uint64_t i) { return !rep || rep[i] == i; };
+  uint64_t bmax = 0;
+  for (uint64_t i = 0; i < n; ++i) bmax = std::max(bmax, blocks_for(len[i]));
+  if (bmax <= (1u << 20)) {
+    std::vector<uint64_t> cnt(bmax + 2, 0);  // bucket j = block count bmax - j
+    for (uint64_t i = 0; i < n; ++i)
+      if (keep(i)) cnt[bmax - blocks_for(len[i]) + 1]++;
+    for (uint64_t j = 0; j <= bmax; ++j) cnt[j + 1] += cnt[j];
+    for (uint64_t i = 0; i < n; ++i)
+      if (keep(i)) order[cnt[bmax - blocks_for(len[i])]++] = (uint32_t)i;
+    return cnt[bmax];
   }
-  tmp.resize(n);
+  uint64_t m = 0;
+  for (uint64_t i = 0; i < n; ++i)
+    if (keep(i)) order[m++] = (uint32_t)i;
+  std::vector<uint32_t> key(n);
+  for (uint64_t i = 0; i < n; ++i)
+    key[i] = 0xffffffffu - (uint32_t)std::min<uint64_t>(blocks_for(len[i]), 0xffffffffu);
+  tmp.resize(m);
   uint32_t* src = order;
   uint32_t* dst = tmp.data();
-  for (uint64_t i = 0; i < n; ++i) src[i] = (uint32_t)i;
   for (int shift = 0; shift < 32; shift += 16) {
     std::vector<uint64_t> cnt(65537, 0);
-    for (uint64_t i = 0; i < n; ++i) cnt[((key[src[i]] >> shift) & 0xffff) + 1]++;
+    for (uint64_t q = 0; q < m; ++q) cnt[((key[src[q]] >> shift) & 0xffff) + 1]++;
     for (int d = 0; d < 65536; ++d) cnt[d + 1] += cnt[d];
-    for (uint64_t i = 0; i < n; ++i) dst[cnt[(key[src[i]] >> shift) & 0xffff]++] = src[i];
+    for (uint64_t q = 0; q < m; ++q) dst[cnt[(key[src[q]] >> shift) & 0xffff]++] = src[q];
     std::swap(src, dst);
   }
   // two passes: result is back in `order`
+  return m;
 }
 
 bool all_equal_blocks(const uint64_t* len, uint64_t n) {
@@ -161,6 +180,22 @@ void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
   bounds[k] = n;
 }
 
+// Per-GPU plan of one host-memory call (kept in the context: its vectors are
+// reused call after call, so planning does not page-fault fresh memory).
+struct Plan {
+  uint64_t m = 0;
+  bool ordered = false;
+  std::vector<uint32_t> perm;       // sorted lane -> shard-local message
+  std::vector<uint64_t> place;      // placement -> shard-local message whose bytes it holds
+  std::vector<uint64_t> ppos;       // placement -> device arena offset (size +1)
+  std::vector<uint64_t> lane_cut;   // chunk boundaries in sorted lanes
+  std::vector<uint64_t> place_cut;  // chunk boundaries in placements
+  size_t next = 0;                  // next chunk to issue
+  uint64_t launched = 0;            // lanes [0, launched) have a kernel enqueued
+  uint64_t lanes = 0;               // messages that get a lane (one per distinct payload)
+  std::vector<uint32_t> rep;        // shard-local message -> its lane's message (empty: identity)
+};
+
 }  // namespace
 
 struct msha_ctx {
@@ -170,6 +205,11 @@ struct msha_ctx {
   std::vector<void*> pinned;  // allocations handed out by msha_pinned_alloc
   std::vector<uint32_t> sort_tmp;
   std::vector<uint64_t> tmp_len;
+  int kernel_policy = MSHA_KERNEL_AUTO;
+  // host planning buffers reused across calls
+  std::vector<Plan> plans;
+  std::vector<uint64_t> uid, placed;
+  std::vector<uint64_t> alias_table;
 };
 
 namespace {
@@ -214,6 +254,55 @@ void parallel_ranges(uint64_t n, uint64_t bytes, F&& f) {
   for (auto& x : th) x.join();
 }
 
+// uid[i] = the first index j <= i with (off[j], len[j]) == (off[i], len[i]).
+// Open addressing (linear probing); an entry is (index + 1) | hash-tag << 32,
+// so a probe dereferences off/len only when the tags match. The table is split
+// into T regions by the key hash's top bits and each region is built by its
+// own thread scanning the keys in index order, so "first" is preserved.
+void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vector<uint64_t>& uid,
+                std::vector<uint64_t>& table) {
+  uid.resize(n);
+  const unsigned T = n >= (1u << 20) ? 8 : 1;
+  const unsigned tbits = T == 8 ? 3 : 0;
+  uint64_t cap = 1;  // per region
+  while (cap * T < 2 * n) cap <<= 1;
+  table.assign(cap * T, 0);  // 0 = empty
+  auto key_hash = [&](uint64_t i) {  // splitmix64 finalizer over both fields
+    uint64_t h = off[i] ^ (len[i] * 0x9E3779B97F4A7C15ull);
+    h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
+    h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
+    return h ^ (h >> 31);
+  };
+  auto build = [&](unsigned t) {
+    uint64_t* reg = table.data() + (uint64_t)t * cap;
+    for (uint64_t i = 0; i < n; ++i) {
+      const uint64_t h = key_hash(i);
+      if (tbits && (h >> (64 - tbits)) != t) continue;
+      const uint64_t tag = h & 0xffffffff00000000ull;
+      for (uint64_t p = h & (cap - 1);; p = (p + 1) & (cap - 1)) {
+        const uint64_t e = reg[p];
+        if (e == 0) {
+          reg[p] = tag | (i + 1);
+          uid[i] = i;
+          break;
+        }
+        const uint64_t j = (e & 0xffffffffull) - 1;
+        if ((e & 0xffffffff00000000ull) == tag && off[j] == off[i] && len[j] == len[i]) {
+          uid[i] = j;
+          break;
+        }
+      }
+    }
+  };
+  if (T == 1) {
+    build(0);
+    return;
+  }
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < T; ++t) th.emplace_back(build, t);
+  for (auto& x : th) x.join();
+}
+
 // Host-memory execution of one batch (the body of every host entry point):
 //   shard messages [0, n) over the context's GPUs by cumulative block count;
 //   per GPU, place its messages in descending-block order (a wave's lanes then
@@ -227,28 +316,27 @@ constexpr uint64_t kChunkBytes = 32ull << 20;
 // uid (may be null): messages with equal uid[i] have identical bytes (aliases,
 // e.g. one EpochChange re-hashed N^2 times, epoch_target.go:486-505); their
 // payload is copied once per GPU.
+// t0: when the entry point was called (plan_ms includes its validation).
 template <class Gather>
-void run_pipeline(msha_ctx* ctx, uint64_t n, const uint64_t* len, const uint64_t* uid, uint8_t* out,
-                  Gather&& gather) {
+void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, const uint64_t* uid,
+                  uint8_t* out, Gather&& gather) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   std::vector<uint64_t> bounds(k + 1);
   partition(len, n, k, bounds.data());
-  double t0 = now_ms(), gather_ms = 0;
+  double gather_ms = 0;
 
-  struct Plan {
-    uint64_t m = 0;
-    bool ordered = false;
-    std::vector<uint32_t> perm;       // sorted lane -> shard-local message
-    std::vector<uint64_t> place;      // placement -> shard-local message whose bytes it holds
-    std::vector<uint64_t> ppos;       // placement -> device arena offset (size +1)
-    std::vector<uint64_t> lane_cut;   // chunk boundaries in sorted lanes
-    std::vector<uint64_t> place_cut;  // chunk boundaries in placements
-    size_t next = 0;                  // next chunk to issue
-  };
-  std::vector<Plan> plans(k);
-  // uid -> placement of its payload in the current shard (UINT64_MAX = none yet)
-  std::vector<uint64_t> placed(uid ? n : 0, UINT64_MAX);
-  std::vector<uint64_t> touched;  // uids placed in the current shard (reset per shard)
+  std::vector<Plan>& plans = ctx->plans;
+  plans.resize(k);
+  for (Plan& P : plans) {
+    P.m = 0;
+    P.next = 0;
+    P.launched = 0;
+  }
+  // uid -> first shard-local message with that payload (UINT64_MAX = none
+  // yet); only needed to find representatives per shard when k > 1
+  std::vector<uint64_t>& placed = ctx->placed;
+  if (uid && k > 1 && placed.size() < n) placed.assign(n, UINT64_MAX);
+  std::vector<uint64_t> touched;  // uids seen in the current shard (reset per shard)
   for (uint32_t s = 0; s < k; ++s) {
     Device& d = ctx->devs[s];
     Plan& P = plans[s];
@@ -257,53 +345,73 @@ void run_pipeline(msha_ctx* ctx, uint64_t n, const uint64_t* len, const uint64_t
     P.m = d.hi - d.lo;
     if (P.m == 0) continue;
     const uint64_t* L = len + d.lo;
-    P.ordered = !all_equal_blocks(L, P.m);
+    // Aliases (same uid) have identical bytes, hence identical digests: only
+    // the first message of each uid gets a lane; the others copy its digest
+    // after the D2H (EpochChange re-hashing, epoch_target.go:486-505).
+    P.rep.clear();
+    P.lanes = P.m;
+    if (uid && k == 1) {  // one shard: uid[i] (the first index with i's payload) is the lane's message
+      P.rep.resize(P.m);
+      P.lanes = 0;
+      for (uint64_t i = 0; i < P.m; ++i) {
+        P.rep[i] = (uint32_t)uid[i];
+        P.lanes += uid[i] == i;
+      }
+      if (P.lanes == P.m) P.rep.clear();
+    } else if (uid) {
+      P.rep.resize(P.m);
+      P.lanes = 0;
+      for (uint64_t i = 0; i < P.m; ++i) {
+        uint64_t& first = placed[uid[d.lo + i]];
+        if (first == UINT64_MAX) {
+          first = i;
+          touched.push_back(uid[d.lo + i]);
+          P.rep[i] = (uint32_t)i;
+          ++P.lanes;
+        } else {
+          P.rep[i] = (uint32_t)first;
+        }
+      }
+      for (uint64_t t : touched) placed[t] = UINT64_MAX;
+      touched.clear();
+      if (P.lanes == P.m) P.rep.clear();
+    }
+    P.perm.resize(P.lanes);
+    if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
+      order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp, P.rep.data());
+      P.ordered = true;
+    } else {
+      P.ordered = !all_equal_blocks(L, P.m);
+      if (P.ordered) order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp);
+      else for (uint64_t i = 0; i < P.m; ++i) P.perm[i] = (uint32_t)i;
+    }
     d.use_order = P.ordered;
-    P.perm.resize(P.m);
-    if (P.ordered) order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp);
-    else for (uint64_t i = 0; i < P.m; ++i) P.perm[i] = (uint32_t)i;
     d.h_meta.ensure(16 * P.m + 4 * P.m);
     uint64_t* h_off = d.h_meta.as<uint64_t>();
     uint64_t* h_len = h_off + P.m;
-    // Place payloads in first-use order of the sorted lanes; aliased messages
-    // (same uid) share one placement, so every lane of chunk c reads bytes
-    // uploaded by the end of chunk c.
-    P.place.clear();
-    P.ppos.clear();
+    // Place payloads in lane order (each lane's payload is distinct: aliases
+    // were folded into their representative above), so every lane of chunk c
+    // reads bytes uploaded by the end of chunk c.
+    P.place.assign(P.perm.begin(), P.perm.begin() + P.lanes);
+    P.ppos.resize(P.lanes);
     P.lane_cut.assign(1, 0);
-    P.place_cut.assign(1, 0);
     uint64_t acc = 0, chunk_start = 0;
-    for (uint64_t q = 0; q < P.m; ++q) {
+    for (uint64_t q = 0; q < P.lanes; ++q) {  // lane-indexed metadata: sequential writes
       const uint32_t i = P.perm[q];
-      uint64_t at;
-      uint64_t* pl = uid ? &placed[uid[d.lo + i]] : nullptr;
-      if (pl && *pl != UINT64_MAX) {
-        at = P.ppos[*pl];
-      } else {
-        if (pl) {
-          *pl = P.place.size();
-          touched.push_back(uid[d.lo + i]);
-        }
-        P.place.push_back(i);
-        P.ppos.push_back(acc);
-        at = acc;
-        acc += round16(L[i]);
-      }
-      h_off[i] = at;
-      h_len[i] = L[i];
-      if (acc - chunk_start >= kChunkBytes && q + 1 < P.m) {
+      P.ppos[q] = acc;
+      h_off[q] = acc;
+      h_len[q] = L[i];
+      acc += round16(L[i]);
+      if (acc - chunk_start >= kChunkBytes && q + 1 < P.lanes) {
         P.lane_cut.push_back(q + 1);
-        P.place_cut.push_back(P.place.size());
         chunk_start = acc;
       }
     }
-    for (uint64_t t : touched) placed[t] = UINT64_MAX;
-    touched.clear();
     P.ppos.push_back(acc);
-    P.lane_cut.push_back(P.m);
-    P.place_cut.push_back(P.place.size());
+    P.lane_cut.push_back(P.lanes);
+    P.place_cut = P.lane_cut;
     d.arena_bytes = acc;
-    if (P.ordered) std::memcpy(h_len + P.m, P.perm.data(), 4 * P.m);
+    if (P.ordered) std::memcpy(h_len + P.m, P.perm.data(), 4 * P.lanes);
     uint64_t slot_bytes = 0;
     for (size_t c = 0; c + 1 < P.place_cut.size(); ++c)
       slot_bytes = std::max(slot_bytes, P.ppos[P.place_cut[c + 1]] - P.ppos[P.place_cut[c]]);
@@ -315,11 +423,11 @@ void run_pipeline(msha_ctx* ctx, uint64_t n, const uint64_t* len, const uint64_t
     d.len.ensure(8 * P.m);
     d.out.ensure(32 * P.m);
     d.err.ensure(4);
-    if (P.ordered) d.order.ensure(4 * P.m);
-    HIPCHK(hipMemcpyAsync(d.off.p, h_off, 8 * P.m, hipMemcpyHostToDevice, d.stream));
-    HIPCHK(hipMemcpyAsync(d.len.p, h_len, 8 * P.m, hipMemcpyHostToDevice, d.stream));
+    if (P.ordered) d.order.ensure(4 * P.lanes);
+    HIPCHK(hipMemcpyAsync(d.off.p, h_off, 8 * P.lanes, hipMemcpyHostToDevice, d.stream));
+    HIPCHK(hipMemcpyAsync(d.len.p, h_len, 8 * P.lanes, hipMemcpyHostToDevice, d.stream));
     if (P.ordered)
-      HIPCHK(hipMemcpyAsync(d.order.p, h_len + P.m, 4 * P.m, hipMemcpyHostToDevice, d.stream));
+      HIPCHK(hipMemcpyAsync(d.order.p, h_len + P.m, 4 * P.lanes, hipMemcpyHostToDevice, d.stream));
     HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
     HIPCHK(hipEventRecord(d.ev0, d.stream));
     HIPCHK(hipEventRecord(d.slot_free[0], d.copy_stream));
@@ -335,7 +443,7 @@ void run_pipeline(msha_ctx* ctx, uint64_t n, const uint64_t* len, const uint64_t
       if (P.m == 0 || P.next + 1 >= P.lane_cut.size()) continue;
       more = true;
       const size_t c = P.next++;
-      const uint64_t q0 = P.lane_cut[c], q1 = P.lane_cut[c + 1];
+      const uint64_t q1 = P.lane_cut[c + 1];
       const uint64_t u0 = P.place_cut[c], u1 = P.place_cut[c + 1];
       const uint64_t b0 = P.ppos[u0], b1 = P.ppos[u1];
       PinBuf& slot = d.slot[c & 1];
@@ -353,17 +461,23 @@ void run_pipeline(msha_ctx* ctx, uint64_t n, const uint64_t* len, const uint64_t
       HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
       HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
       HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
-      const uint64_t lanes = q1 - q0;
-      if (P.ordered) {
-        HIPCHK(msha::launch_digest_batch(d.arena.as<uint8_t>(), d.off.as<uint64_t>(),
-                                         d.len.as<uint64_t>(), d.order.as<uint32_t>() + q0, lanes,
-                                         d.out.as<uint8_t>(), d.err.as<uint32_t>(), d.cus, d.stream));
-      } else {  // identity placement: lane q hashes message q
-        HIPCHK(msha::launch_digest_batch(d.arena.as<uint8_t>(), d.off.as<uint64_t>() + q0,
-                                         d.len.as<uint64_t>() + q0, nullptr, lanes,
-                                         d.out.as<uint8_t>() + 32 * q0, d.err.as<uint32_t>(), d.cus,
-                                         d.stream));
-      }
+      // Kernels are launched over the lanes accumulated since the last launch
+      // once they fill the GPU (2 waves per SIMD) or at the last chunk: hashing
+      // runs ~30x faster than PCIe delivers bytes, so a launch per 32 MiB chunk
+      // would only buy overlap worth a few % while a chunk of large messages
+      // (512 x 64 KiB) leaves most SIMDs idle for the whole of its long chains.
+      const bool last = P.next + 1 >= P.lane_cut.size();
+      const uint64_t fill = (uint64_t)d.cus * 4 * 64 * 2;
+      if (!last && q1 - P.launched < fill) continue;
+      const uint64_t l0 = P.launched, lanes = q1 - l0;
+      P.launched = q1;
+      // off/len are lane-indexed; out_idx maps lane -> shard-local message
+      // (identity placement: lane q is message q)
+      HIPCHK(msha::launch_digest_batch(
+          d.arena.as<uint8_t>(), d.off.as<uint64_t>() + l0, d.len.as<uint64_t>() + l0, nullptr,
+          P.ordered ? d.order.as<uint32_t>() + l0 : nullptr, lanes,
+          d.out.as<uint8_t>() + (P.ordered ? 0 : 32 * l0), d.err.as<uint32_t>(), d.cus,
+          ctx->kernel_policy, d.stream));
     }
   }
   for (uint32_t s = 0; s < k; ++s) {
@@ -389,7 +503,13 @@ void run_pipeline(msha_ctx* ctx, uint64_t n, const uint64_t* len, const uint64_t
     uint32_t errflag;
     std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
     if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
-    std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
+    const std::vector<uint32_t>& rep = plans[s].rep;
+    if (rep.empty()) {
+      std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
+    } else {
+      const uint8_t* h = d.h_out.as<uint8_t>();
+      for (uint64_t i = 0; i < m; ++i) std::memcpy(out + 32 * (d.lo + i), h + 32 * (uint64_t)rep[i], 32);
+    }
   }
   ctx->stats.calls++;
   ctx->stats.plan_ms = t_plan - t0;
@@ -512,47 +632,26 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
   if (n == 0) return MSHA_OK;
   if (!off || !len || !out || (arena_len && !arena))
     return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
-  for (uint64_t i = 0; i < n; ++i)
-    if (len[i] > arena_len || off[i] > arena_len - len[i])
-      return fail(ctx, MSHA_ERR_INVALID_ARG,
-                  "message " + std::to_string(i) + " [off+len] outside arena");
+  if (n >= 0xffffffffull) return fail(ctx, MSHA_ERR_INVALID_ARG, "more than 2^32-2 messages in one call");
+  const double t0 = now_ms();
   return guarded(ctx, [&] {
-    // Overlapping payloads (sum of lengths > the span they cover) means aliases:
-    // give every message the index of the first message with the same (off, len).
-    uint64_t lo = UINT64_MAX, hi = 0, sum = 0;
+    // One pass: bounds, the covered span, total bytes and blocks.
+    uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0;
     for (uint64_t i = 0; i < n; ++i) {
+      if (len[i] > arena_len || off[i] > arena_len - len[i])
+        throw MshaError(MSHA_ERR_INVALID_ARG, "message " + std::to_string(i) + " [off+len] outside arena");
       lo = std::min(lo, off[i]);
       hi = std::max(hi, off[i] + len[i]);
       sum += len[i];
+      blocks += blocks_for(len[i]);
     }
-    std::vector<uint64_t> uidv;
-    if (n > 1 && sum > hi - lo) {
-      // open-addressing table (linear probing) of first index + 1 per (off, len)
-      uint64_t cap = 1;
-      while (cap < 2 * n) cap <<= 1;
-      std::vector<uint64_t> table(cap, 0);
-      uidv.resize(n);
-      for (uint64_t i = 0; i < n; ++i) {
-        uint64_t hsh = (off[i] * 0x9E3779B97F4A7C15ull) ^ (len[i] * 0xC2B2AE3D27D4EB4Full);
-        hsh ^= hsh >> 29;
-        for (uint64_t p = hsh & (cap - 1);; p = (p + 1) & (cap - 1)) {
-          const uint64_t e = table[p];
-          if (e == 0) {
-            table[p] = i + 1;
-            uidv[i] = i;
-            break;
-          }
-          if (off[e - 1] == off[i] && len[e - 1] == len[i]) {
-            uidv[i] = e - 1;
-            break;
-          }
-        }
-      }
-    }
-    run_pipeline(ctx, n, len, uidv.empty() ? nullptr : uidv.data(), out,
+    // Overlapping payloads (sum of lengths > the span they cover) means there
+    // may be aliases: give every message the index of the first message with
+    // the same (off, len).
+    const bool aliases = n > 1 && sum > hi - lo;
+    if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table);
+    run_pipeline(ctx, t0, n, len, aliases ? ctx->uid.data() : nullptr, out,
                  [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); });
-    uint64_t blocks = 0;
-    for (uint64_t i = 0; i < n; ++i) blocks += blocks_for(len[i]);
     ctx->stats.messages += n;
     ctx->stats.message_bytes += sum;
     ctx->stats.blocks += blocks;
@@ -574,13 +673,14 @@ int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
   for (uint64_t j = 0; j < n_parts; ++j)
     if (part_len[j] > arena_len || part_off[j] > arena_len - part_len[j])
       return fail(ctx, MSHA_ERR_INVALID_ARG, "part " + std::to_string(j) + " outside arena");
+  const double t0 = now_ms();
   return guarded(ctx, [&] {
     // Message length of each action = sum of its parts (h.Write appends).
     std::vector<uint64_t>& alen = ctx->tmp_len;
     alen.assign(n_actions, 0);
     for (uint64_t i = 0; i < n_actions; ++i)
       for (uint64_t j = action_part_begin[i]; j < action_part_begin[i + 1]; ++j) alen[i] += part_len[j];
-    run_pipeline(ctx, n_actions, alen.data(), nullptr, out, [&](uint64_t a, uint8_t* dst) {
+    run_pipeline(ctx, t0, n_actions, alen.data(), nullptr, out, [&](uint64_t a, uint8_t* dst) {
       for (uint64_t j = action_part_begin[a]; j < action_part_begin[a + 1]; ++j) {
         std::memcpy(dst, arena + part_off[j], part_len[j]);
         dst += part_len[j];
@@ -684,8 +784,8 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
     hipStream_t st;
     device_prologue(ctx, stream, &st);
     Device& d = ctx->devs[0];
-    HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, d_order, n, d_out, d.err.as<uint32_t>(),
-                                     d.cus, st));
+    HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, d_order, nullptr, n, d_out,
+                                     d.err.as<uint32_t>(), d.cus, ctx->kernel_policy, st));
   });
 }
 
@@ -713,6 +813,14 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
     device_prologue(ctx, stream, &st);
     HIPCHK(msha::launch_digest_of_digests(d_table, d_idx, d_begin, n, d_out, st));
   });
+}
+
+int msha_set_kernel_policy(msha_ctx* ctx, int policy) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (policy != MSHA_KERNEL_AUTO && policy != MSHA_KERNEL_LANE && policy != MSHA_KERNEL_COOP)
+    return fail(ctx, MSHA_ERR_INVALID_ARG, "unknown kernel policy " + std::to_string(policy));
+  ctx->kernel_policy = policy;
+  return MSHA_OK;
 }
 
 int msha_device_status(msha_ctx* ctx) {

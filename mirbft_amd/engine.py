@@ -92,19 +92,29 @@ class Engine:
         if rc != L.MSHA_OK:
             raise MshaError(rc, self._lib.msha_last_error(self._ctx).decode())
 
+    def set_kernel_policy(self, policy: str) -> None:
+        """"auto" (default), "lane" (one lane per message) or "coop" (cooperative chaining)."""
+        code = {"auto": L.MSHA_KERNEL_AUTO, "lane": L.MSHA_KERNEL_LANE, "coop": L.MSHA_KERNEL_COOP}[policy]
+        self._check(self._lib.msha_set_kernel_policy(self._ctx, code))
+
     def stats(self) -> dict:
         s = L.MshaStats()
         self._check(self._lib.msha_get_stats(self._ctx, ctypes.byref(s)))
         return {name: getattr(s, name) for name, _ in L.MshaStats._fields_}
 
     # -- host-memory entry points -----------------------------------------
-    def digest_batch(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray) -> np.ndarray:
-        """out[i] = SHA-256(arena[off[i] : off[i]+len[i]]) -> uint8 [n, 32]."""
+    def digest_batch(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray,
+                     out: Optional[np.ndarray] = None) -> np.ndarray:
+        """out[i] = SHA-256(arena[off[i] : off[i]+len[i]]) -> uint8 [n, 32]
+        (``out``: an optional caller-owned C-contiguous uint8 [n, 32] result buffer)."""
         arena = np.ascontiguousarray(arena, dtype=np.uint8).reshape(-1)
         off = np.ascontiguousarray(off, dtype=np.uint64)
         length = np.ascontiguousarray(length, dtype=np.uint64)
         n = off.size
-        out = np.empty((n, 32), dtype=np.uint8)
+        if out is None:
+            out = np.empty((n, 32), dtype=np.uint8)
+        elif out.shape != (n, 32) or out.dtype != np.uint8 or not out.flags.c_contiguous:
+            raise ValueError("out must be a C-contiguous uint8 array of shape (n, 32)")
         if n == 0:
             return out
         ap = arena if arena.size else np.zeros(1, dtype=np.uint8)

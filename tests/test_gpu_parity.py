@@ -135,6 +135,20 @@ def test_aliased_payloads(engine):
         assert g.tobytes() == exp[k]
 
 
+def test_alias_dedup_keys_on_offset_and_length(engine):
+    """Hash dedup is per (off, len): a shared start with different lengths, or
+    equal bytes at different offsets, are distinct lanes; repeats copy digests."""
+    base = bytes(np.random.default_rng(3).integers(0, 256, 5000, dtype=np.uint8))
+    arena = np.zeros(2 * 5008 + 64, dtype=np.uint8)
+    arena[:5000] = np.frombuffer(base, dtype=np.uint8)
+    arena[5008:10008] = np.frombuffer(base, dtype=np.uint8)
+    off = np.array([0, 0, 0, 5008, 0, 16, 0], dtype=np.uint64)
+    ln = np.array([5000, 4999, 5000, 5000, 0, 100, 5000], dtype=np.uint64)
+    got = engine.digest_batch(arena, off, ln)
+    for g, o, n_ in zip(got, off, ln):
+        assert g.tobytes() == hashlib.sha256(arena[int(o):int(o + n_)].tobytes()).digest()
+
+
 def test_mixed_sizes_many_lanes(engine):
     """> 3 waves/SIMD of mixed sizes: non-prefetch kernel + size-class ordering."""
     n = 250_000

@@ -1,0 +1,64 @@
+// Host-only timing of the planning steps of msha_digest_batch on a c5-shaped
+// batch (8M messages: 70% 512 B, 25% k x 32 B, 5% aliases of 100 ~49 KB
+// payloads). No GPU: the helpers are compiled straight from mirsha.cpp.
+// Build: hipcc -O3 -std=c++17 -o tools/plan_bench tools/plan_bench.cpp -lpthread
+#include "../mirbft_amd/csrc/mirsha.cpp"
+
+#include <cstdio>
+#include <random>
+
+// The launchers live in kernels.hip; this host-only harness never launches.
+namespace msha {
+hipError_t launch_digest_batch(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*,
+                               const uint32_t*, uint64_t, uint8_t*, uint32_t*, int, int, hipStream_t) {
+  return hipErrorNotSupported;
+}
+hipError_t launch_digest_of_digests(const uint8_t*, const uint32_t*, const uint64_t*, uint64_t, uint8_t*,
+                                    hipStream_t) {
+  return hipErrorNotSupported;
+}
+hipError_t launch_digest_uniform(const uint8_t*, uint64_t, uint64_t, uint64_t, uint8_t*, uint32_t*, int,
+                                 hipStream_t) {
+  return hipErrorNotSupported;
+}
+}  // namespace msha
+
+int main(int argc, char** argv) {
+  const uint64_t n = argc > 1 ? strtoull(argv[1], nullptr, 0) : (1ull << 23);
+  std::vector<uint64_t> off(n), len(n);
+  std::mt19937_64 rng(1);
+  uint64_t pool_off[100], pool_len[100], pos = 0;
+  for (int j = 0; j < 100; ++j) { pool_len[j] = 30000 + rng() % 40000; pool_off[j] = pos; pos += round16(pool_len[j]); }
+  for (uint64_t i = 0; i < n; ++i) {
+    const double r = (rng() >> 11) * 0x1.0p-53;
+    if (r < 0.95) { len[i] = r < 0.70 ? 512 : 32 * (1 + rng() % 20); off[i] = pos; pos += round16(len[i]); }
+    else { const int j = rng() % 100; off[i] = pool_off[j]; len[i] = pool_len[j]; }
+  }
+  auto T = [](const char* what, double t0) { std::printf("%-28s %8.1f ms\n", what, now_ms() - t0); return now_ms(); };
+  double t = now_ms();
+  uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0;
+  for (uint64_t i = 0; i < n; ++i) {
+    if (len[i] > pos || off[i] > pos - len[i]) return 1;
+    lo = std::min(lo, off[i]); hi = std::max(hi, off[i] + len[i]); sum += len[i]; blocks += blocks_for(len[i]);
+  }
+  t = T("validate+span+blocks", t);
+  std::vector<uint64_t> uid;
+  std::vector<uint64_t> table;
+  for (int rep_i = 0; rep_i < 2; ++rep_i) {  // second round: buffers warm (as in a context)
+    alias_uids(off.data(), len.data(), n, uid, table);
+    t = T("alias_uids", t);
+  }
+  std::vector<uint32_t> rep(n);
+  uint64_t lanes = 0;
+  for (uint64_t i = 0; i < n; ++i) { rep[i] = (uint32_t)uid[i]; lanes += uid[i] == i; }
+  t = T("rep", t);
+  std::vector<uint32_t> perm(lanes), tmp;
+  order_by_blocks_desc(len.data(), n, perm.data(), tmp, rep.data());
+  t = T("order_by_blocks_desc(subset)", t);
+  std::vector<uint64_t> h_off(lanes), h_len(lanes), ppos(lanes);
+  uint64_t acc = 0;
+  for (uint64_t q = 0; q < lanes; ++q) { const uint32_t i = perm[q]; ppos[q] = acc; h_off[q] = acc; h_len[q] = len[i]; acc += round16(len[i]); }
+  t = T("placement", t);
+  std::printf("n=%llu lanes=%llu\n", (unsigned long long)n, (unsigned long long)lanes);
+  return 0;
+}
