@@ -7,11 +7,11 @@ reference's ``processor.Hasher`` / ``ProcessHashActions`` surface.
 from .engine import Engine, MshaError, blocks_for_len, device_count, pack_parts, partition_by_blocks
 from .processor import (Action, ActionHashRequest, ActionList, EventHashResult, EventList, GPUHasher,
                         HashOrigin, HashOriginBatch, HashOriginEpochChange, HashOriginVerifyBatch,
-                        ProcessHashActions, ProcessorError, action_hash)
+                        ProcessHashActions, ProcessorError, action_hash, checkpoint_hashes)
 
 __all__ = [
     "Engine", "MshaError", "blocks_for_len", "device_count", "pack_parts", "partition_by_blocks",
     "Action", "ActionHashRequest", "ActionList", "EventHashResult", "EventList", "GPUHasher",
     "HashOrigin", "HashOriginBatch", "HashOriginEpochChange", "HashOriginVerifyBatch",
-    "ProcessHashActions", "ProcessorError", "action_hash",
+    "ProcessHashActions", "ProcessorError", "action_hash", "checkpoint_hashes",
 ]

@@ -9,6 +9,8 @@ kernels.
 * VerifyBatch    applyForwardBatchMsg      /root/reference/pkg/statemachine/batch_tracker.go:175-188
 * EpochChange    epochChangeHashData       /root/reference/pkg/statemachine/stateless.go:323-352
                  uint64ToBytes (BIG-endian) /root/reference/pkg/statemachine/proposer.go:16-20
+* checkpoint value (app-level running hash)  NodeState.Snap/Apply/TransferTo
+                 /root/reference/pkg/testengine/recorder.go:288-353 (New at :420)
 * testengine request payload  RequestByReqNo  /root/reference/pkg/testengine/recorder.go:258-270
                  uint64ToBytes (LITTLE-endian) /root/reference/pkg/testengine/recorder.go:33-37
 """
@@ -90,3 +92,13 @@ def epoch_change_hash_data(ec: EpochChange) -> List[bytes]:
 def recorder_request_bytes(client_id: int, req_no: int) -> Optional[bytes]:
     """RecorderClient.RequestByReqNo payload: LE64(client) ++ '-' ++ LE64(reqNo) (17 bytes)."""
     return uint64_to_bytes_le(client_id) + b"-" + uint64_to_bytes_le(req_no)
+
+
+def checkpoint_hash_data(prev_checkpoint_hash: Optional[bytes], committed_digests: List[bytes]) -> List[bytes]:
+    """Everything NodeState.ActiveHash has been written with when Snap takes its
+    Sum (recorder.go:288-300): the previous CheckpointHash (written right after
+    the previous Snap, :299-300, or by TransferTo, :326-328; absent for the
+    first interval, whose ActiveHash is a fresh Hasher.New(), :420), then the
+    digest of every request Apply committed since, in commit order (:348)."""
+    head = [] if prev_checkpoint_hash is None else [prev_checkpoint_hash]
+    return head + list(committed_digests)

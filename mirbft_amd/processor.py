@@ -28,7 +28,7 @@ from typing import Any, Iterator, List, Optional, Sequence, Union
 
 import numpy as np
 
-from .encoding import EpochChange, RequestAck
+from .encoding import EpochChange, RequestAck, checkpoint_hash_data
 from .engine import Engine
 
 
@@ -199,6 +199,32 @@ class GPUHasher:
         arena = np.frombuffer(b"".join(bytes(r) for r in requests), dtype=np.uint8)
         out = self.engine.digest_batch(arena, offs, lens)
         return [bytes(r) for r in out]
+
+
+def checkpoint_hashes(hasher: GPUHasher, intervals: Sequence[tuple]) -> List[bytes]:
+    """the testengine's app-level checkpoint value
+    (NodeState.Snap, recorder.go:288-300) for many (node, interval) pairs in one
+    GPU call. intervals[i] = (prev_checkpoint_hash or None, [committed request
+    digests]); result[i] = ActiveHash.Sum(nil) at Snap = SHA-256 of
+    checkpoint_hash_data(prev, digests). Every part is a 32-byte digest, so this
+    is the digest-of-digests kernel over one table of all parts. A node's
+    successive intervals form a chain (each starts from the previous result), so
+    the batch dimension is across nodes / ready intervals."""
+    if not intervals:
+        return []
+    parts: List[bytes] = []
+    begin = [0]
+    for prev, digests in intervals:
+        for d in checkpoint_hash_data(prev, list(digests)):
+            if len(d) != 32:
+                raise ProcessorError("checkpoint_hashes: every part must be a 32-byte digest")
+            parts.append(bytes(d))
+        begin.append(len(parts))
+    table = np.frombuffer(b"".join(parts), dtype=np.uint8).reshape(-1, 32) if parts \
+        else np.zeros((0, 32), dtype=np.uint8)
+    idx = np.arange(len(parts), dtype=np.uint32)
+    out = hasher.engine.digest_of_digests(table, idx, np.array(begin, dtype=np.uint64))
+    return [bytes(r) for r in out]
 
 
 def ProcessHashActions(hasher: GPUHasher, actions: ActionList) -> EventList:

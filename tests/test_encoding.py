@@ -71,3 +71,40 @@ def test_process_hash_actions_non_hash_action_error():
     al = ActionList([Action(type="send")])
     with pytest.raises(ProcessorError, match="unexpected type for Hash action"):
         ProcessHashActions(FakeHasher(), al)
+
+
+class _NodeState:
+    """Streaming restatement of testengine NodeState's ActiveHash (recorder.go:288-353, :420)
+    with hashlib: the oracle for checkpoint_hash_data."""
+
+    def __init__(self):
+        import hashlib
+        self._h = hashlib.sha256()           # Hasher.New() (recorder.go:420)
+        self.checkpoint_hash = None
+
+    def apply(self, digests):
+        for d in digests:                     # ActiveHash.Write(request.Digest) (:348)
+            self._h.update(d)
+
+    def snap(self):
+        import hashlib
+        self.checkpoint_hash = self._h.digest()   # ActiveHash.Sum(nil) (:298)
+        self._h = hashlib.sha256()
+        self._h.update(self.checkpoint_hash)      # (:299-300)
+        return self.checkpoint_hash
+
+
+def test_checkpoint_hash_data_matches_streaming_active_hash():
+    import hashlib
+    import random
+    from mirbft_amd.encoding import checkpoint_hash_data
+    rnd = random.Random(7)
+    ns = _NodeState()
+    prev = None
+    for interval in range(6):
+        digests = [hashlib.sha256(bytes([interval, j])).digest() for j in range(rnd.randrange(0, 9))]
+        ns.apply(digests)
+        expect = ns.snap()
+        data = checkpoint_hash_data(prev, digests)
+        assert hashlib.sha256(b"".join(data)).digest() == expect
+        prev = expect
