@@ -27,3 +27,8 @@ if [[ $STEPS == all || $STEPS == *prof* ]]; then
   find gpurun_out/prof -name "*kernel_stats*" | head -3
   for f in $(find gpurun_out/prof -name "*kernel_stats.csv"); do cat $f; done
 fi
+if [[ $STEPS == *dist* ]]; then
+  # 2-rank rehearsal of the torchrun path on a 1-GPU box (both ranks on GPU 0)
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --share-device --no-cpu-baseline > gpurun_out/bench_dist2.json 2> gpurun_out/bench_dist2.err; stop_on_fault $? dist2
+  cat gpurun_out/bench_dist2.json
+fi
