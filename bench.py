@@ -34,6 +34,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 OPS_PER_BLOCK = 1400           # DESIGN.md "Algorithmic work per block"
+# Best rate this instruction mix reaches on register-resident data (no HBM):
+# 28.3 G blocks/s x 1400 (tools/valu_microbench4.hip, profiles/r01_valu_microbench4.jsonl)
+ISA_MIX_CEILING_TOPS = 28.3e9 * OPS_PER_BLOCK / 1e12
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T int32 lane-ops/s
 METRIC = "SHA-256 digests/sec + GB/s hashed (1/2/4/8 MI355X), % integer-ALU roofline"
 
@@ -55,6 +58,9 @@ def parse():
                         "same workload; prints an end-to-end line (never the headline value)")
     p.add_argument("--policy", default="auto", choices=["auto", "lane", "coop"],
                    help="batch-kernel policy (msha_set_kernel_policy); digests are identical")
+    p.add_argument("--pinned", action="store_true",
+                   help="with --e2e: the batch is packed in pinned host memory (msha_pinned_alloc), "
+                        "as a cgo adapter would, so the library DMAs it as is")
     p.add_argument("--share-device", action="store_true",
                    help="rehearsal only: every rank uses GPU 0 (multi-rank path on a 1-GPU box)")
     return p.parse_args()
@@ -88,26 +94,52 @@ def build_workload(cfg: str, rank: int, world: int):
     raise ValueError(cfg)
 
 
+def _time_cpu(fn, n: int, nbytes_per: int, seconds: float):
+    done = nbytes = 0
+    t0 = time.perf_counter()
+    while True:
+        fn()
+        done += n
+        nbytes += nbytes_per
+        el = time.perf_counter() - t0
+        if el >= seconds:
+            return done / el, nbytes / el / 1e9, done, el
+
+
+CPU_THREADS = 16   # the GPU box's CPU share per GPU
+
+
 def cpu_baseline(w, seconds: float):
-    """Oracle (scalar C, 1 thread) on a bounded prefix sample of the same workload."""
+    """Oracle (scalar C, 1 thread: the reference's single hash goroutine, mirbft.go:470)
+    on a bounded prefix sample of the same workload; plus the strongest CPU numbers:
+    OpenSSL libcrypto (SHA-NI) on 1 and CPU_THREADS threads, same sample shape."""
     from oracle import oracle
     oracle.lib()
     n = min(w.n, 4096)
     off, ln = w.off[:n], w.len[:n]
-    done = 0
-    nbytes = 0
-    t0 = time.perf_counter()
-    while True:
-        oracle.digest_batch(w.arena, off, ln)
-        done += n
-        nbytes += int(ln.sum())
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": done / el, "unit": "digests/s", "cores": 1, "kind": "port",
-            "gbps": nbytes / el / 1e9,
+    per = int(ln.sum())
+    v, g, done, el = _time_cpu(lambda: oracle.digest_batch(w.arena, off, ln), n, per, seconds)
+    line = {"value": v, "unit": "digests/s", "cores": 1, "kind": "port", "gbps": g,
             "sample": f"first {n} messages of the same workload, repeated for {el:.1f} s "
                       f"({done} digests), oracle/sha256_oracle.c single thread"}
+    try:
+        import platform
+        cpu = next((l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")),
+                   platform.processor())
+        sha_ni = " sha_ni " in open("/proc/cpuinfo").read().replace("\n", " ")
+        v1, g1, _, _ = _time_cpu(lambda: oracle.openssl_digest_batch(w.arena, off, ln, 1), n, per, seconds / 2)
+        m = min(w.n, 4096 * CPU_THREADS)
+        offm, lnm = w.off[:m], w.len[:m]
+        vt, gt, _, _ = _time_cpu(lambda: oracle.openssl_digest_batch(w.arena, offm, lnm, CPU_THREADS), m,
+                                 int(lnm.sum()), seconds / 2)
+        line["openssl"] = {"cpu": cpu, "sha_ni": sha_ni,
+                           "1_thread": {"value": v1, "gbps": g1},
+                           f"{CPU_THREADS}_threads": {"value": vt, "gbps": gt},
+                           "source": "oracle/sha256_openssl.c (EVP_Digest), stronger than the reference's "
+                                     "Go 1.15/1.16 crypto/sha256 (no SHA-NI path)"}
+    except (OSError, RuntimeError) as e:   # libcrypto missing: report the port only
+        line["openssl"] = {"error": str(e)}
+    return line
 
 
 TRAFFIC_FILE = "profiles/r01_traffic.json"
@@ -136,11 +168,15 @@ def verify_sample(w, d_out, k: int = 512) -> None:
 def run_e2e(args, eng, w, world):
     """End-to-end host path: numpy arena in pageable host memory -> digests in host memory."""
     out = np.empty((w.n, 32), dtype=np.uint8)   # a node reuses its result buffer
+    arena = w.arena
+    if args.pinned:
+        arena = eng.pinned_empty(w.arena.size)
+        arena[:] = w.arena
     for _ in range(max(1, args.warmup)):
-        eng.digest_batch(w.arena, w.off, w.len, out=out)
+        eng.digest_batch(arena, w.off, w.len, out=out)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.digest_batch(w.arena, w.off, w.len, out=out)
+        eng.digest_batch(arena, w.off, w.len, out=out)
     el = time.perf_counter() - t0
     st = eng.stats()
     from oracle import oracle
@@ -148,6 +184,7 @@ def run_e2e(args, eng, w, world):
     if not np.array_equal(out[sel], oracle.digest_batch(w.arena, w.off[sel], w.len[sel])):
         raise SystemExit("e2e output mismatch vs oracle")
     print(json.dumps({"metric": "end-to-end host API (pack + H2D + kernel + D2H), NOT the headline",
+                      "arena": "pinned (msha_pinned_alloc)" if args.pinned else "pageable numpy",
                       "value": w.n * args.steps / el, "unit": "digests/s", "n_gpus": world,
                       "gbps_hashed": w.message_bytes * args.steps / el / 1e9,
                       "ms_per_step": el / args.steps * 1e3, "config": {"workload": w.name},
@@ -275,7 +312,9 @@ def main():
                                  "v_add3) and costs ~4 SIMD cycles per instruction on gfx950, so the "
                                  "ISA-mix ceiling measured on a register-resident loop is ~0.50 of "
                                  "this peak (DESIGN.md, profiles/r01_valu_microbench*)",
-                         "algorithmic_bytes_per_launch": w.message_bytes + 32 * w.n + 16 * w.n},
+                         "algorithmic_bytes_per_launch": w.message_bytes + 32 * w.n + 16 * w.n,
+                         "isa_mix_ceiling": ISA_MIX_CEILING_TOPS,
+                         "frac_of_isa_mix_ceiling": achieved / ISA_MIX_CEILING_TOPS},
         }
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)

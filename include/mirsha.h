@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 1u
+#define MSHA_ABI_VERSION 2u
 
 enum {
   MSHA_OK = 0,
@@ -72,6 +72,7 @@ typedef struct {
   double pack_ms;          /* gathering payload bytes into pinned staging (threads) */
   double device_ms;        /* first upload .. last kernel on the device (HIP events, max over GPUs) */
   double total_ms;         /* whole call */
+  uint64_t direct_calls;   /* host calls whose arena was uploaded as is (pinned, 16-B aligned) */
 } msha_stats;
 
 uint32_t msha_abi_version(void);
@@ -161,7 +162,10 @@ int msha_device_status(msha_ctx* ctx);
 enum { MSHA_KERNEL_AUTO = 0, MSHA_KERNEL_LANE = 1, MSHA_KERNEL_COOP = 2 };
 int msha_set_kernel_policy(msha_ctx* ctx, int policy);
 
-/* Pinned host memory for callers that want zero-copy staging. */
+/* Pinned host memory for callers that want zero-copy staging: when the arena
+ * passed to msha_digest_batch lies in such memory, every message start is
+ * 16-byte aligned and the messages are packed without large gaps, each GPU's
+ * byte span of it is DMA'd as is (no gather copy into the library's staging). */
 int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p);
 int msha_pinned_free(msha_ctx* ctx, void* p);
 

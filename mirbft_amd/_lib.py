@@ -14,6 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
+ABI_VERSION = 2
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -42,6 +43,7 @@ class MshaStats(ctypes.Structure):
         ("pack_ms", ctypes.c_double),
         ("device_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double),
+        ("direct_calls", ctypes.c_uint64),
     ]
 
 
@@ -109,7 +111,7 @@ def lib() -> ctypes.CDLL:
         fn = getattr(L, name)
         fn.restype = res
         fn.argtypes = args
-    if L.msha_abi_version() != 1:
+    if L.msha_abi_version() != ABI_VERSION:
         raise ImportError("libmirsha ABI version mismatch")
     _lib = L
     return L

@@ -103,6 +103,7 @@ struct Device {
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
+  uint64_t direct_lo = 0;         // direct mode: first caller-arena byte uploaded
   bool use_order = false;
   void release() {
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table}) b->release();
@@ -254,6 +255,17 @@ void parallel_ranges(uint64_t n, uint64_t bytes, F&& f) {
   for (auto& x : th) x.join();
 }
 
+// Is p inside page-locked host memory the GPU can DMA from (hipHostMalloc /
+// hipHostRegister)? Pageable memory makes the query fail; clear that error.
+bool is_pinned_host(const void* p) {
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
 // uid[i] = the first index j <= i with (off[j], len[j]) == (off[i], len[i]).
 // Open addressing (linear probing); an entry is (index + 1) | hash-tag << 32,
 // so a probe dereferences off/len only when the tags match. The table is split
@@ -317,9 +329,18 @@ constexpr uint64_t kChunkBytes = 32ull << 20;
 // e.g. one EpochChange re-hashed N^2 times, epoch_target.go:486-505); their
 // payload is copied once per GPU.
 // t0: when the entry point was called (plan_ms includes its validation).
+// direct (may be null): the caller's arena is pinned host memory whose message
+// starts are 16-byte aligned (msha_pinned_alloc); then each GPU's byte span of
+// it is DMA'd as is (no gather copy, no re-placement) and off/len index into
+// that span.
+struct Direct {
+  const uint8_t* arena;
+  const uint64_t* off;
+};
+
 template <class Gather>
 void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, const uint64_t* uid,
-                  uint8_t* out, Gather&& gather) {
+                  uint8_t* out, Gather&& gather, const Direct* direct = nullptr) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   std::vector<uint64_t> bounds(k + 1);
   partition(len, n, k, bounds.data());
@@ -392,31 +413,53 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     // Place payloads in lane order (each lane's payload is distinct: aliases
     // were folded into their representative above), so every lane of chunk c
     // reads bytes uploaded by the end of chunk c.
-    P.place.assign(P.perm.begin(), P.perm.begin() + P.lanes);
-    P.ppos.resize(P.lanes);
-    P.lane_cut.assign(1, 0);
-    uint64_t acc = 0, chunk_start = 0;
-    for (uint64_t q = 0; q < P.lanes; ++q) {  // lane-indexed metadata: sequential writes
-      const uint32_t i = P.perm[q];
-      P.ppos[q] = acc;
-      h_off[q] = acc;
-      h_len[q] = L[i];
-      acc += round16(L[i]);
-      if (acc - chunk_start >= kChunkBytes && q + 1 < P.lanes) {
-        P.lane_cut.push_back(q + 1);
-        chunk_start = acc;
+    uint64_t acc = 0;
+    if (direct) {  // the shard's span of the caller's pinned arena, uploaded as is
+      uint64_t lo = UINT64_MAX, hi = 0;
+      for (uint64_t q = 0; q < P.lanes; ++q) {
+        const uint32_t i = P.perm[q];
+        lo = std::min(lo, direct->off[d.lo + i]);
+        hi = std::max(hi, direct->off[d.lo + i] + L[i]);
       }
+      for (uint64_t q = 0; q < P.lanes; ++q) {
+        const uint32_t i = P.perm[q];
+        h_off[q] = direct->off[d.lo + i] - lo;
+        h_len[q] = L[i];
+      }
+      d.direct_lo = lo;
+      acc = hi - lo;
+      P.place.clear();
+      P.ppos.assign({0, acc});
+      P.lane_cut.assign({0, P.lanes});
+    } else {
+      P.place.assign(P.perm.begin(), P.perm.begin() + P.lanes);
+      P.ppos.resize(P.lanes);
+      P.lane_cut.assign(1, 0);
+      uint64_t chunk_start = 0;
+      for (uint64_t q = 0; q < P.lanes; ++q) {  // lane-indexed metadata: sequential writes
+        const uint32_t i = P.perm[q];
+        P.ppos[q] = acc;
+        h_off[q] = acc;
+        h_len[q] = L[i];
+        acc += round16(L[i]);
+        if (acc - chunk_start >= kChunkBytes && q + 1 < P.lanes) {
+          P.lane_cut.push_back(q + 1);
+          chunk_start = acc;
+        }
+      }
+      P.ppos.push_back(acc);
+      P.lane_cut.push_back(P.lanes);
     }
-    P.ppos.push_back(acc);
-    P.lane_cut.push_back(P.lanes);
     P.place_cut = P.lane_cut;
     d.arena_bytes = acc;
     if (P.ordered) std::memcpy(h_len + P.m, P.perm.data(), 4 * P.lanes);
-    uint64_t slot_bytes = 0;
-    for (size_t c = 0; c + 1 < P.place_cut.size(); ++c)
-      slot_bytes = std::max(slot_bytes, P.ppos[P.place_cut[c + 1]] - P.ppos[P.place_cut[c]]);
-    d.slot[0].ensure(std::max<uint64_t>(slot_bytes, 16));
-    d.slot[1].ensure(std::max<uint64_t>(slot_bytes, 16));
+    if (!direct) {
+      uint64_t slot_bytes = 0;
+      for (size_t c = 0; c + 1 < P.place_cut.size(); ++c)
+        slot_bytes = std::max(slot_bytes, P.ppos[P.place_cut[c + 1]] - P.ppos[P.place_cut[c]]);
+      d.slot[0].ensure(std::max<uint64_t>(slot_bytes, 16));
+      d.slot[1].ensure(std::max<uint64_t>(slot_bytes, 16));
+    }
     HIPCHK(hipSetDevice(d.id));
     d.arena.ensure(acc + msha::kArenaSlack);
     d.off.ensure(8 * P.m);
@@ -445,19 +488,25 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       const size_t c = P.next++;
       const uint64_t q1 = P.lane_cut[c + 1];
       const uint64_t u0 = P.place_cut[c], u1 = P.place_cut[c + 1];
-      const uint64_t b0 = P.ppos[u0], b1 = P.ppos[u1];
+      const uint64_t b0 = direct ? 0 : P.ppos[u0], b1 = direct ? d.arena_bytes : P.ppos[u1];
       PinBuf& slot = d.slot[c & 1];
       HIPCHK(hipSetDevice(d.id));
-      HIPCHK(hipEventSynchronize(d.slot_free[c & 1]));   // its previous H2D has drained
-      const double g0 = now_ms();
-      uint8_t* dst = slot.as<uint8_t>();
-      parallel_ranges(u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
-        for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.place[u], dst + (P.ppos[u] - b0));
-      });
-      gather_ms += now_ms() - g0;
-      if (b1 > b0)
-        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
-                              d.copy_stream));
+      if (direct) {
+        if (b1 > b0)
+          HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>(), direct->arena + d.direct_lo, b1 - b0,
+                                hipMemcpyHostToDevice, d.copy_stream));
+      } else {
+        HIPCHK(hipEventSynchronize(d.slot_free[c & 1]));   // its previous H2D has drained
+        const double g0 = now_ms();
+        uint8_t* dst = slot.as<uint8_t>();
+        parallel_ranges(u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
+          for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.place[u], dst + (P.ppos[u] - b0));
+        });
+        gather_ms += now_ms() - g0;
+        if (b1 > b0)
+          HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
+                                d.copy_stream));
+      }
       HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
       HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
       HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
@@ -636,22 +685,31 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
   const double t0 = now_ms();
   return guarded(ctx, [&] {
     // One pass: bounds, the covered span, total bytes and blocks.
-    uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0;
+    uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0, offbits = reinterpret_cast<uintptr_t>(arena);
     for (uint64_t i = 0; i < n; ++i) {
       if (len[i] > arena_len || off[i] > arena_len - len[i])
         throw MshaError(MSHA_ERR_INVALID_ARG, "message " + std::to_string(i) + " [off+len] outside arena");
+      offbits |= off[i];
       lo = std::min(lo, off[i]);
       hi = std::max(hi, off[i] + len[i]);
       sum += len[i];
       blocks += blocks_for(len[i]);
     }
+    const bool aligned16 = (offbits & 15) == 0;
     // Overlapping payloads (sum of lengths > the span they cover) means there
     // may be aliases: give every message the index of the first message with
     // the same (off, len).
     const bool aliases = n > 1 && sum > hi - lo;
     if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table);
+    // Zero-copy upload when the caller packed into pinned memory (msha_pinned_alloc)
+    // with 16-byte aligned message starts and little waste between messages.
+    Direct dir{arena, off};
+    const bool direct = aligned16 && hi - lo <= std::min(sum, hi - lo) + 16 * n + (1u << 20) &&
+                        is_pinned_host(arena + lo);
     run_pipeline(ctx, t0, n, len, aliases ? ctx->uid.data() : nullptr, out,
-                 [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); });
+                 [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); },
+                 direct ? &dir : nullptr);
+    ctx->stats.direct_calls += direct;
     ctx->stats.messages += n;
     ctx->stats.message_bytes += sum;
     ctx->stats.blocks += blocks;

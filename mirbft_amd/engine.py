@@ -73,8 +73,23 @@ class Engine:
     # -- lifecycle -------------------------------------------------------
     def close(self) -> None:
         if getattr(self, "_ctx", None):
+            for p in getattr(self, "_pinned", []):
+                self._lib.msha_pinned_free(self._ctx, p)
+            self._pinned = []
             self._lib.msha_ctx_destroy(self._ctx)
             self._ctx = None
+
+    def pinned_empty(self, nbytes: int) -> np.ndarray:
+        """A uint8 numpy array in page-locked host memory (msha_pinned_alloc).
+        Packing a batch into it (16-byte aligned message starts) lets
+        digest_batch DMA it as is. Valid until close()."""
+        p = ctypes.c_void_p()
+        self._check(self._lib.msha_pinned_alloc(self._ctx, max(int(nbytes), 1), ctypes.byref(p)))
+        if not hasattr(self, "_pinned"):
+            self._pinned = []
+        self._pinned.append(p.value)
+        buf = (ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value)
+        return np.frombuffer(buf, dtype=np.uint8, count=int(nbytes))
 
     def __enter__(self):
         return self

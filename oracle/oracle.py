@@ -11,6 +11,9 @@ against the committed FIPS 180-4 known answers (tests/golden/kat.json):
   restating ``processor.ProcessHashActions`` (/root/reference/pkg/processor/serial.go:180-198)
   over Go ``crypto/sha256`` (FIPS 180-4; Go stdlib, not in the reference tree).
 * ``py_sha256`` below: a pure-Python FIPS 180-4 restatement, for small inputs.
+* ``liboracle_openssl.so`` built from ``oracle/sha256_openssl.c``: the same loop
+  over OpenSSL libcrypto (SHA-NI where the CPU has it), multi-threaded; a third
+  cross-check and bench.py's strongest CPU baseline.
 
 The reference itself (Go) cannot be built or run in this image (no ``go``), so
 parity is pinned by the FIPS 180-4 known-answer vectors plus an independent
@@ -27,7 +30,9 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "build", "liboracle_sha256.so")
+_SSL_PATH = os.path.join(_HERE, "build", "liboracle_openssl.so")
 _lib = None
+_ssl = None
 
 
 def build() -> str:
@@ -54,6 +59,38 @@ def lib():
             f.restype = None
         _lib = L
     return _lib
+
+
+def ssl_lib():
+    global _ssl
+    if _ssl is None:
+        if not os.path.exists(_SSL_PATH):
+            build()
+        L = ctypes.CDLL(_SSL_PATH)
+        L.openssl_digest_batch.argtypes = [ctypes.POINTER(ctypes.c_uint8), ctypes.POINTER(ctypes.c_uint64),
+                                           ctypes.POINTER(ctypes.c_uint64), ctypes.c_uint64,
+                                           ctypes.POINTER(ctypes.c_uint8), ctypes.c_int]
+        L.openssl_digest_batch.restype = ctypes.c_int
+        _ssl = L
+    return _ssl
+
+
+def openssl_digest_batch(arena: np.ndarray, off: np.ndarray, length: np.ndarray, threads: int = 1) -> np.ndarray:
+    """digest_batch via OpenSSL libcrypto over `threads` threads; uint8 [n, 32]."""
+    arena = np.ascontiguousarray(arena, dtype=np.uint8)
+    if arena.size == 0:
+        arena = np.zeros(1, dtype=np.uint8)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint64)
+    n = off.size
+    out = np.zeros((n, 32), dtype=np.uint8)
+    if n == 0:
+        return out
+    rc = ssl_lib().openssl_digest_batch(_p(arena, ctypes.c_uint8), _p(off, ctypes.c_uint64),
+                                        _p(length, ctypes.c_uint64), n, _p(out, ctypes.c_uint8), threads)
+    if rc != 0:
+        raise RuntimeError("openssl_digest_batch failed")
+    return out
 
 
 def _p(a: np.ndarray, t):

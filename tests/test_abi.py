@@ -29,7 +29,7 @@ def test_exports_via_nm():
 
 
 def test_abi_version():
-    assert L.lib().msha_abi_version() == 1
+    assert L.lib().msha_abi_version() == L.ABI_VERSION == 2
 
 
 def test_library_is_gfx950_code_object():

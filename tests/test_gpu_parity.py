@@ -361,3 +361,26 @@ def test_missing_device_in_mask_is_an_error():
     with pytest.raises(MshaError) as ei:
         Engine(1 << n)          # one past the last visible device
     assert ei.value.code == L.MSHA_ERR_NO_DEVICE
+
+
+def test_pinned_arena_direct_upload(engine):
+    """A batch packed in msha_pinned_alloc memory with 16-B aligned starts is DMA'd
+    as is (stats.direct_calls); misaligned or gappy layouts take the gather path.
+    Digests identical either way, with aliases and mixed sizes."""
+    w = W.c5_storm(1 << 14)
+    pinned = engine.pinned_empty(w.arena.size)
+    pinned[:] = w.arena
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    before = engine.stats()["direct_calls"]
+    assert np.array_equal(engine.digest_batch(pinned, w.off, w.len), exp)
+    assert engine.stats()["direct_calls"] == before + 1
+    # an unaligned start: gather path, same digests
+    off2 = w.off.copy()
+    pinned2 = engine.pinned_empty(w.arena.size + 16)
+    pinned2[8:8 + w.arena.size] = w.arena
+    off2 += 8
+    assert np.array_equal(engine.digest_batch(pinned2, off2, w.len), exp)
+    assert engine.stats()["direct_calls"] == before + 1
+    # pageable memory: gather path
+    assert np.array_equal(engine.digest_batch(w.arena, w.off, w.len), exp)
+    assert engine.stats()["direct_calls"] == before + 1

@@ -69,3 +69,16 @@ def test_digest_of_digests_oracle():
 def test_random_lengths_vs_hashlib(L):
     m = np.random.default_rng(L).integers(0, 256, L, dtype=np.uint8).tobytes()
     assert oracle.sha256(m) == hashlib.sha256(m).digest()
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+def test_openssl_oracle_matches_c_oracle(lengths_golden, threads):
+    """Third restatement (OpenSSL libcrypto, threaded ranges) == scalar C oracle == fixtures."""
+    msgs = [m for m, _ in lengths_golden]
+    lens = np.array([len(m) for m in msgs], dtype=np.uint64)
+    off = np.zeros(len(msgs), dtype=np.uint64)
+    off[1:] = np.cumsum(lens)[:-1]
+    arena = np.frombuffer(b"".join(msgs) + b"\0", dtype=np.uint8)
+    got = oracle.openssl_digest_batch(arena, off, lens, threads=threads)
+    assert np.array_equal(got, oracle.digest_batch(arena, off, lens))
+    assert [g.tobytes() for g in got] == [d for _, d in lengths_golden]
