@@ -15,7 +15,8 @@
 // object (shared_ptr identity, the Go pointer), and fails with
 // "unexpected type for Hash action: <type>" on a non-hash action
 // (serial.go:192-194). The difference is the engine: the whole list is hashed
-// by one msha_hash_actions() call (one H2D, one launch per GPU, one D2H).
+// by one msha_digest_batch() call over a pinned, 16-byte aligned arena
+// (one H2D DMA, one launch per GPU, one D2H).
 #pragma once
 
 #include <cstdint>
@@ -144,83 +145,94 @@ class GPUHasher {
     if (int rc = msha_ctx_create(device_mask, &ctx_); rc != MSHA_OK)
       throw std::runtime_error(std::string("libmirsha: ") + msha_last_error(nullptr));
   }
-  ~GPUHasher() { msha_ctx_destroy(ctx_); }
+  ~GPUHasher() {
+    if (pinned_) msha_pinned_free(ctx_, pinned_);
+    msha_ctx_destroy(ctx_);
+  }
   GPUHasher(const GPUHasher&) = delete;
   GPUHasher& operator=(const GPUHasher&) = delete;
 
   GPUHash New() { return GPUHash(this); }
 
-  // One digest per message = SHA-256(concat(parts)), in order.
+  // One digest per message = SHA-256(concat(parts)), in order. Each message's
+  // parts are packed back to back (h.Write appends), every message starting
+  // 16-byte aligned, into the context's pinned arena: libmirsha uploads it as
+  // is (msha_pinned_alloc / msha_stats.direct_calls), one msha_digest_batch.
   Result<std::vector<Bytes>> HashBatch(const std::vector<const std::vector<Bytes>*>& msgs) {
     Result<std::vector<Bytes>> r;
-    size_t n_parts = 0, n_bytes = 0;
+    size_t n_bytes = 0;
     for (auto* m : msgs) {
-      n_parts += m->size();
       for (auto& p : *m) n_bytes += p.size();
+      n_bytes += 15;
     }
-    // Pack [][]byte into one arena + offsets: the layout the C ABI takes.
-    Bytes arena(n_bytes + 1);
-    std::vector<uint64_t> off(n_parts + 1), len(n_parts + 1), begin(msgs.size() + 1);
-    size_t pos = 0, j = 0;
+    std::vector<uint64_t> off(msgs.size() + 1), len(msgs.size() + 1);
+    uint8_t* arena = nullptr;
+    if (!PinnedArena(n_bytes + 64, &arena, &r.err)) return r;
+    size_t pos = 0;
     for (size_t i = 0; i < msgs.size(); ++i) {
-      begin[i] = j;
+      off[i] = pos;
       for (auto& p : *msgs[i]) {
-        if (!p.empty()) std::memcpy(arena.data() + pos, p.data(), p.size());
-        off[j] = pos;
-        len[j] = p.size();
+        if (!p.empty()) std::memcpy(arena + pos, p.data(), p.size());
         pos += p.size();
-        ++j;
       }
+      len[i] = pos - off[i];
+      pos = (pos + 15) & ~size_t(15);
     }
-    begin[msgs.size()] = j;
-    Bytes out(32 * msgs.size());
-    if (!msgs.empty()) {
-      int rc = msha_hash_actions(ctx_, arena.data(), n_bytes, off.data(), len.data(), n_parts,
-                                 begin.data(), msgs.size(), out.data());
-      if (rc != MSHA_OK) {
-        r.err = "libmirsha error " + std::to_string(rc) + ": " + msha_last_error(ctx_);
-        return r;
-      }
-    }
-    r.value.reserve(msgs.size());
-    for (size_t i = 0; i < msgs.size(); ++i)  // fresh copies: the state machine keeps digests
-      r.value.emplace_back(out.begin() + 32 * i, out.begin() + 32 * (i + 1));
-    return r;
+    return Digest(arena, pos, off, len, msgs.size());
   }
 
   // Batched request intake: Client.Propose's per-call digest
   // (clients.go:189-192) for a whole batch of proposals, one msha_digest_batch.
   Result<std::vector<Bytes>> RequestDigests(const std::vector<Bytes>& requests) {
-    Result<std::vector<Bytes>> r;
-    size_t total = 0;
-    for (auto& q : requests) total += q.size();
-    Bytes arena(total + 1);
-    std::vector<uint64_t> off(requests.size() + 1), len(requests.size() + 1);
-    size_t pos = 0;
+    std::vector<std::vector<Bytes>> one(requests.size());
+    std::vector<const std::vector<Bytes>*> msgs(requests.size());
     for (size_t i = 0; i < requests.size(); ++i) {
-      if (!requests[i].empty()) std::memcpy(arena.data() + pos, requests[i].data(), requests[i].size());
-      off[i] = pos;
-      len[i] = requests[i].size();
-      pos += requests[i].size();
+      one[i].push_back(requests[i]);
+      msgs[i] = &one[i];
     }
-    Bytes out(32 * requests.size());
-    if (!requests.empty()) {
-      int rc = msha_digest_batch(ctx_, arena.data(), total, off.data(), len.data(), requests.size(),
-                                 out.data());
-      if (rc != MSHA_OK) {
-        r.err = "libmirsha error " + std::to_string(rc) + ": " + msha_last_error(ctx_);
-        return r;
-      }
-    }
-    for (size_t i = 0; i < requests.size(); ++i)
-      r.value.emplace_back(out.begin() + 32 * i, out.begin() + 32 * (i + 1));
-    return r;
+    return HashBatch(msgs);
   }
 
   msha_ctx* ctx() { return ctx_; }
 
  private:
+  // The context's pinned packing arena, grown on demand.
+  bool PinnedArena(size_t bytes, uint8_t** p, std::string* err) {
+    if (bytes > pinned_cap_) {
+      if (pinned_) msha_pinned_free(ctx_, pinned_);
+      pinned_ = nullptr;
+      pinned_cap_ = 0;
+      const size_t want = bytes + bytes / 4 + 4096;
+      if (int rc = msha_pinned_alloc(ctx_, want, &pinned_); rc != MSHA_OK) {
+        *err = "libmirsha error " + std::to_string(rc) + ": " + msha_last_error(ctx_);
+        return false;
+      }
+      pinned_cap_ = want;
+    }
+    *p = static_cast<uint8_t*>(pinned_);
+    return true;
+  }
+
+  Result<std::vector<Bytes>> Digest(const uint8_t* arena, size_t arena_len, const std::vector<uint64_t>& off,
+                                    const std::vector<uint64_t>& len, size_t n) {
+    Result<std::vector<Bytes>> r;
+    Bytes out(32 * n);
+    if (n) {
+      int rc = msha_digest_batch(ctx_, arena, arena_len, off.data(), len.data(), n, out.data());
+      if (rc != MSHA_OK) {
+        r.err = "libmirsha error " + std::to_string(rc) + ": " + msha_last_error(ctx_);
+        return r;
+      }
+    }
+    r.value.reserve(n);
+    for (size_t i = 0; i < n; ++i)  // fresh copies: the state machine keeps digests
+      r.value.emplace_back(out.begin() + 32 * i, out.begin() + 32 * (i + 1));
+    return r;
+  }
+
   msha_ctx* ctx_ = nullptr;
+  void* pinned_ = nullptr;
+  size_t pinned_cap_ = 0;
 };
 
 inline Bytes GPUHash::Sum(Bytes b) const {

@@ -107,6 +107,18 @@ int main() {
     for (size_t i = 0; i < reqs.size() && i < r.value.size(); ++i)
       EXPECT(r.value[i] == oracle({reqs[i]}), "request digest == oracle");
   }
+  {  // It("packs the list into a pinned, 16-byte aligned arena that libmirsha uploads as is")
+    msha_stats before{}, after{};
+    msha_get_stats(hasher.ctx(), &before);
+    ActionList al;
+    for (int i = 0; i < 300; ++i) al.Hash({Bytes(i % 97, (uint8_t)i), Bytes(i % 13, 7)}, nullptr);
+    auto r = processor::ProcessHashActions(hasher, al);
+    EXPECT(r.ok(), "no error");
+    msha_get_stats(hasher.ctx(), &after);
+    EXPECT(after.direct_calls == before.direct_calls + 1, "direct (zero-copy) upload");
+    for (int i = 0; i < 300; ++i)
+      EXPECT(r.value.Items()[i].digest == oracle({Bytes(i % 97, (uint8_t)i), Bytes(i % 13, 7)}), "digest");
+  }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;
