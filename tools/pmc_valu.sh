@@ -1,0 +1,29 @@
+#!/bin/bash
+# PMC passes per config (separate rocprofv3 runs, --kernel-trace + --pmc only):
+#   sq    : VALU/SALU instruction counts, VALU-active and wave cycles, waits, clock (GRBM)
+#   sq2   : INT32 VALU instructions, integer ops, VALU thread-cycles, SALU cycles, LDS instrs
+#   fetch : FETCH_SIZE        write : WRITE_SIZE   (HBM bytes, gfx950 recipe)
+# -> gpurun_out/pmc/<cfg>_<pass>/run_counter_collection.csv; summarise with
+#    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc.json
+set -u
+export TMPDIR=/tmp
+OUT=gpurun_out/pmc
+mkdir -p $OUT
+prof() {  # name, counters, cmd...
+  local name=$1 ctr=$2; shift 2
+  timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $ctr --output-format csv -d $OUT/$name -o run -- "$@" > $OUT/$name.log 2>&1
+  local rc=$?; echo "$name rc=$rc"; [ $rc -ge 124 ] && exit $rc; return 0
+}
+SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
+SQ2="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_IOPS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+PASSES=${PASSES:-sq sq2 fetch write}
+for spec in ${SPECS:-c2:auto c3:auto c3dd:auto c4:auto c5:auto ub_16384_65536:coop ub_16384_65536:lane}; do
+  cfg=${spec%%:*}; pol=${spec##*:}; arg=$(echo $cfg | tr '_' ':')
+  name=${cfg}_${pol}
+  cmd="python3 bench.py --config $arg --policy $pol --steps 3 --warmup 1 --no-cpu-baseline"
+  [[ $PASSES == *"sq "* || $PASSES == sq ]] && prof ${name}_sq "$SQ" $cmd
+  [[ $PASSES == *sq2* ]] && prof ${name}_sq2 "$SQ2" $cmd
+  [[ $PASSES == *fetch* ]] && prof ${name}_fetch FETCH_SIZE $cmd
+  [[ $PASSES == *write* ]] && prof ${name}_write WRITE_SIZE $cmd
+done
+exit 0
