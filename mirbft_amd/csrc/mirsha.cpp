@@ -317,17 +317,21 @@ void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vecto
 
 // Host-memory execution of one batch (the body of every host entry point):
 //   shard messages [0, n) over the context's GPUs by cumulative block count;
-//   per GPU, place its messages in descending-block order (a wave's lanes then
-//   run equal block counts) at 16-byte aligned offsets of the device arena,
-//   upload off/len(/order), and stream the payload in chunks through two pinned
-//   staging slots: host threads gather chunk c+1 while chunk c's H2D and kernel
-//   run (copy stream -> event -> kernel stream). Digests come back with one D2H
-//   per GPU at the end. gather(i, dst) copies message i's bytes to dst.
+//   per GPU, give one lane to each distinct payload (aliases fold into their
+//   first occurrence), order lanes by descending block count (a wave's lanes
+//   then run equal block counts), place the payloads at 16-byte aligned
+//   offsets of the device arena, upload lane-indexed off/len + the lane ->
+//   message map, and stream the payload in chunks through two pinned staging
+//   slots: host threads gather chunk c+1 while chunk c's H2D runs on the copy
+//   stream. Kernels (compute stream, event-ordered after their chunks) run over
+//   accumulated chunks once these fill the GPU, or at the last chunk. Digests
+//   come back with one D2H per GPU; aliases copy their representative's.
+//   gather(i, dst) copies message i's bytes to dst.
 constexpr uint64_t kChunkBytes = 32ull << 20;
 
 // uid (may be null): messages with equal uid[i] have identical bytes (aliases,
 // e.g. one EpochChange re-hashed N^2 times, epoch_target.go:486-505); their
-// payload is copied once per GPU.
+// payload is copied and hashed once per GPU.
 // t0: when the entry point was called (plan_ms includes its validation).
 // direct (may be null): the caller's arena is pinned host memory whose message
 // starts are 16-byte aligned (msha_pinned_alloc); then each GPU's byte span of
