@@ -71,10 +71,11 @@ def test_device_unordered_mixed_blocks(eng):
     assert np.array_equal(out.cpu().numpy(), oracle.digest_batch(arena, off, lens))
 
 
-def test_device_ordered_c5(eng):
+@pytest.mark.parametrize("n", [1 << 14, 40_000])   # coop: latency form (G=2) / balanced form (G=4)
+def test_device_ordered_c5(eng, n):
     import torch
     from mirbft_amd.engine import order_by_blocks
-    w = W.c5_storm(1 << 14)
+    w = W.c5_storm(n)
     out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
     order = _dev(order_by_blocks(w.len).view(np.int32))
     eng.digest_batch_device(_dev(w.arena), _dev(w.off), _dev(w.len), out, order=order)
