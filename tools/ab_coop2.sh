@@ -1,6 +1,7 @@
 #!/bin/bash
 # A/B of the batch kernels around one wave per SIMD: lane vs cooperative
-# latency form (G=2) vs balanced form (G=4).
+# latency form (G=2) vs balanced form (G=4). The G=4 form (MSHA_COOP_G) was
+# removed after this A/B (profiles/r01_ab_coop2/: no gain over the lane kernel).
 set -u
 OUT=${OUT:-gpurun_out/ab_coop2}
 mkdir -p $OUT
