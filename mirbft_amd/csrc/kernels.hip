@@ -25,19 +25,13 @@
 
 namespace msha {
 
-// Mode bit 4 (kNT): payload loads carry the nontemporal (streaming) cache
-// policy -- every payload byte is read exactly once.
-constexpr int kNT = 4;
-
 template <int MODE = 0>
 __device__ __forceinline__ void load_block16(const uint8_t* p, uint32_t (&raw)[16]) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
   const u32x4* q = reinterpret_cast<const u32x4*>(p);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    u32x4 v;
-    if (MODE & kNT) v = __builtin_nontemporal_load(q + i);
-    else v = q[i];
+    const u32x4 v = q[i];
     raw[4 * i + 0] = v.x; raw[4 * i + 1] = v.y; raw[4 * i + 2] = v.z; raw[4 * i + 3] = v.w;
   }
 }
@@ -56,35 +50,9 @@ __device__ __forceinline__ void to_words(const uint32_t (&raw)[16], uint32_t (&w
 //            128-byte line are requested back to back, so the line is read
 //            from HBM once instead of being evicted and re-fetched between
 //            the two half-line requests (lane stride >= 128 B is the norm)
-//  kLds      LDS-DMA prefetch: block b+1 lands in the wave's 4 KiB LDS slice
-//            (global_load_lds, no VGPR destination) while block b is
-//            compressed, then comes back with four ds_read_b128
-enum LoadMode { kSingle = 0, kPrefetch = 1, kPair = 2, kLds = 3 };
-
-// kLds slice layout: chunk-major [4 chunks][64 lanes] x 16 B, which is what
-// global_load_lds writes (lane l of instruction c lands at c*1 KiB + 16*l) and
-// makes each ds_read_b128 (lane l reads 16 consecutive bytes at c*1 KiB + 16*l)
-// bank-conflict free.
-__device__ __forceinline__ void lds_issue(const uint8_t* pb, uint8_t* lds_wave) {
-  // The previous block's ds_reads of this slice must have completed.
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(pb + 16 * c),
-                                     (__attribute__((address_space(3))) void*)(lds_wave + 1024 * c),
-                                     16, 0, 0);
-}
-
-__device__ __forceinline__ void lds_take(const uint8_t* lds_wave, uint32_t (&raw)[16]) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's LDS-DMA has landed
-  const unsigned lane = threadIdx.x & 63;
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    const u32x4 v = *reinterpret_cast<const u32x4*>(lds_wave + 1024 * c + 16 * lane);
-    raw[4 * c + 0] = v.x; raw[4 * c + 1] = v.y; raw[4 * c + 2] = v.z; raw[4 * c + 3] = v.w;
-  }
-}
+// (Rejected after A/B, profiles/r01_ab_modes, r01_ab_nt: an LDS-DMA prefetch
+// mode, 6 % slower on c2, and nontemporal payload loads, 5-10 % slower.)
+enum LoadMode { kSingle = 0, kPrefetch = 1, kPair = 2 };
 
 // Hash one message of `len` bytes starting at p (device memory, 16-byte
 // aligned, with kArenaSlack (kernels.hpp) readable bytes after the arena's last
@@ -93,8 +61,7 @@ __device__ __forceinline__ void lds_take(const uint8_t* lds_wave, uint32_t (&raw
 // The tail block is read as a whole 64-byte block (it may run into the next
 // message or the slack); build_tail() masks every byte at or past `len`.
 template <int MODE>
-__device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uint8_t* out,
-                                             uint8_t* lds_wave = nullptr) {
+__device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uint8_t* out) {
   State s;
   state_init(s);
   const uint32_t nfull = (uint32_t)(len >> 6);  // < 2^32 blocks: messages < 256 GiB
@@ -112,15 +79,10 @@ __device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uin
   const uint32_t nvalu = nblocks - (upad ? 1 : 0);
   uint32_t raw[16];
   uint32_t w[16];
-  constexpr int LM = MODE & 3;  // load mode; MODE & kNT selects the cache policy
+  constexpr int LM = MODE;  // load mode
   if (LM == kPrefetch) load_block16<MODE>(p, raw);
-  if (LM == kLds && nvalu > 0) lds_issue(p, lds_wave);
   for (uint32_t b = 0; b < nvalu; ++b) {
     const uint8_t* pb = p + 64 * (uint64_t)b;
-    if (LM == kLds) {
-      if (b <= nfull) lds_take(lds_wave, raw);
-      if (b + 1 < nvalu && b + 1 <= nfull) lds_issue(pb + 64, lds_wave);
-    }
     if (LM == kSingle && b <= nfull) load_block16<MODE>(pb, raw);
     if (LM == kPair && b == nfull && !(b & 1)) load_block16<MODE>(pb, raw);
     if (b < nfull) {
@@ -173,16 +135,13 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
                                                       const uint32_t* __restrict__ out_idx,
                                                       uint64_t n, uint8_t* __restrict__ out,
                                                       uint32_t* __restrict__ err) {
-  // kLds: one 4 KiB LDS slice per wave (16 KiB per 256-thread workgroup,
-  // 128 KiB per CU at 8 workgroups)
-  __shared__ __attribute__((aligned(16))) uint8_t lds[(MODE & 3) == kLds ? 4 * 4096 : 16];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint64_t m = order ? (uint64_t)order[i] : i;      // metadata index
   const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;  // digest slot
   const uint8_t* p = arena + off[m];
   if (check_aligned(p, out + 32 * o, err))
-    hash_message<MODE>(p, len[m], out + 32 * o, lds + 4096 * (threadIdx.x / 64));
+    hash_message<MODE>(p, len[m], out + 32 * o);
 }
 
 // ---------------------------------------------------------------------------
@@ -332,12 +291,11 @@ __global__ __launch_bounds__(256, 8) void k_digest_uniform(const uint8_t* __rest
                                                         uint64_t stride, uint64_t msg_len,
                                                         uint64_t n, uint8_t* __restrict__ out,
                                                         uint32_t* __restrict__ err) {
-  __shared__ __attribute__((aligned(16))) uint8_t lds[(MODE & 3) == kLds ? 4 * 4096 : 16];
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   const uint8_t* p = arena + i * stride;
   if (check_aligned(p, out + 32 * i, err))
-    hash_message<MODE>(p, msg_len, out + 32 * i, lds + 4096 * (threadIdx.x / 64));
+    hash_message<MODE>(p, msg_len, out + 32 * i);
 }
 
 // Digest-of-digests (Batch / VerifyBatch actions, /root/reference/pkg/statemachine/
@@ -395,18 +353,15 @@ static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256)
 
 // Fewer than ~3 waves per SIMD cannot hide HBM latency by occupancy: use the
 // register-prefetching variant then; otherwise pair loads. For A/B
-// measurements MSHA_LOAD_MODE (0/1/2) forces the load mode and MSHA_NT=1 the
-// nontemporal payload loads.
+// measurements MSHA_LOAD_MODE (0/1/2) forces the load mode.
 static inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
 static inline int pick_mode(uint64_t n, int cus) {
   static const int forced = env_int("MSHA_LOAD_MODE", -1);
-  static const int nt = env_int("MSHA_NT", 0) ? kNT : 0;
-  const int lm = (forced >= 0 && forced <= 3) ? forced
-                 : (n < (uint64_t)cus * 4 * 64 * 3 ? kPrefetch : kPair);
-  return lm | nt;
+  if (forced >= kSingle && forced <= kPair) return forced;
+  return n < (uint64_t)cus * 4 * 64 * 3 ? kPrefetch : kPair;
 }
 
 // Cooperative chaining (AUTO) when every workgroup of the launch gets a CU of
@@ -426,11 +381,7 @@ static inline void with_mode(int mode, F&& f) {
   switch (mode) {
     case kSingle: f(std::integral_constant<int, kSingle>()); break;
     case kPrefetch: f(std::integral_constant<int, kPrefetch>()); break;
-    case kPair: f(std::integral_constant<int, kPair>()); break;
-    case kLds: f(std::integral_constant<int, kLds>()); break;
-    case kSingle | kNT: f(std::integral_constant<int, kSingle | kNT>()); break;
-    case kPrefetch | kNT: f(std::integral_constant<int, kPrefetch | kNT>()); break;
-    default: f(std::integral_constant<int, kPair | kNT>()); break;
+    default: f(std::integral_constant<int, kPair>()); break;
   }
 }
 
@@ -440,10 +391,8 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
   if (n == 0) return hipSuccess;
   if (uses_coop(n, cus, policy)) {
     const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
-    if (env_int("MSHA_NT", 0))
-      hipLaunchKernelGGL(k_digest_coop<kNT>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len, order, out_idx, n, out, err);
-    else
-      hipLaunchKernelGGL(k_digest_coop<0>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len, order, out_idx, n, out, err);
+    hipLaunchKernelGGL(k_digest_coop<kPrefetch>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len,
+                       order, out_idx, n, out, err);
     return hipGetLastError();
   }
   with_mode(pick_mode(n, cus), [&](auto m) {

@@ -1,7 +1,7 @@
 #!/bin/bash
 # Interleaved A/B of environment-selected kernel variants, per config.
 #   VARIANTS="MSHA_X2=0 MSHA_X2=1" CONFIGS="c2 c3" REPS=2 OUT=gpurun_out/ab_x2 bash tools/ab_env.sh
-# Each variant is one env assignment (or several joined by ','), e.g. "MSHA_X2=1,MSHA_NT=1".
+# Each variant is one env assignment (or several joined by ','), e.g. "MSHA_LOAD_MODE=1,MSHA_X2=1".
 set -u
 OUT=${OUT:-gpurun_out/ab_env}
 mkdir -p $OUT

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of the kernel load modes (MSHA_LOAD_MODE 0..3), interleaved, per config.
+# (Mode 3, LDS-DMA prefetch, was removed after this A/B: profiles/r01_ab_modes/.)
 set -u
 mkdir -p gpurun_out/ab
 export TMPDIR=/tmp

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B: nontemporal payload loads (MSHA_NT=1) vs default, interleaved.
+# (The nontemporal variant was removed after this A/B: profiles/r01_ab_nt/.)
 set -u
 mkdir -p gpurun_out/ab_nt
 for rep in 1 2 3; do
