@@ -293,7 +293,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.config == "c5" else "weak",  # c5: 8M actions per node
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (splitmix64 seed 0x4D49524246540000), inputs resident in HBM",
