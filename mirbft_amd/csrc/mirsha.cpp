@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
@@ -118,6 +119,31 @@ struct Device {
   }
 };
 
+// MSHA_TRACE=1: host-side phase timestamps (ms since the call began) on stderr.
+inline void trace(const char* what, double t0) {
+  static const bool on = getenv("MSHA_TRACE") != nullptr;
+  if (on) fprintf(stderr, "[msha] %-24s %9.2f ms\n", what, now_ms() - t0);
+}
+
+// Host planning of large batches runs on a few threads: [0, n) is split into
+// T contiguous chunks and f(t, lo, hi) runs for each (T = 1 below 256 K items).
+inline unsigned plan_threads(uint64_t n) {
+  if (n < (1u << 18)) return 1;
+  const unsigned hw = std::thread::hardware_concurrency();
+  return std::max(1u, std::min(16u, hw));
+}
+template <class F>
+void parallel_chunks(uint64_t n, unsigned T, F&& f) {
+  if (T <= 1) {
+    f(0u, (uint64_t)0, n);
+    return;
+  }
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (unsigned t = 0; t < T; ++t) th.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
+  for (auto& x : th) x.join();
+}
+
 // Descending-block-count permutation so every wavefront gets messages of equal
 // length and no lane idles. Stable. Batches rarely hold more than a few dozen
 // distinct block counts, so a one-pass counting sort over [0, max blocks]
@@ -128,16 +154,37 @@ struct Device {
 uint64_t order_by_blocks_desc(const uint64_t* len, uint64_t n, uint32_t* order,
                               std::vector<uint32_t>& tmp, const uint32_t* rep = nullptr) {
   auto keep = [&](uint64_t i) { return !rep || rep[i] == i; };
-  uint64_t bmax = 0;
-  for (uint64_t i = 0; i < n; ++i) bmax = std::max(bmax, blocks_for(len[i]));
+  const unsigned T0 = plan_threads(n);
+  std::vector<uint64_t> tmax(T0, 0);
+  parallel_chunks(n, T0, [&](unsigned t, uint64_t lo, uint64_t hi) {
+    uint64_t b = 0;
+    for (uint64_t i = lo; i < hi; ++i) b = std::max(b, blocks_for(len[i]));
+    tmax[t] = b;
+  });
+  const uint64_t bmax = *std::max_element(tmax.begin(), tmax.end());
   if (bmax <= (1u << 20)) {
-    std::vector<uint64_t> cnt(bmax + 2, 0);  // bucket j = block count bmax - j
-    for (uint64_t i = 0; i < n; ++i)
-      if (keep(i)) cnt[bmax - blocks_for(len[i]) + 1]++;
-    for (uint64_t j = 0; j <= bmax; ++j) cnt[j + 1] += cnt[j];
-    for (uint64_t i = 0; i < n; ++i)
-      if (keep(i)) order[cnt[bmax - blocks_for(len[i])]++] = (uint32_t)i;
-    return cnt[bmax];
+    // per-thread histograms only while they stay small
+    const unsigned T = bmax <= (1u << 16) ? T0 : 1;
+    const uint64_t B = bmax + 1;               // bucket j = block count bmax - j
+    std::vector<uint64_t> cnt((uint64_t)T * B, 0);
+    parallel_chunks(n, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+      uint64_t* c = cnt.data() + (uint64_t)t * B;
+      for (uint64_t i = lo; i < hi; ++i)
+        if (keep(i)) c[bmax - blocks_for(len[i])]++;
+    });
+    uint64_t run = 0;  // stable: bucket-major, then thread (= index) order
+    for (uint64_t j = 0; j < B; ++j)
+      for (unsigned t = 0; t < T; ++t) {
+        const uint64_t c = cnt[(uint64_t)t * B + j];
+        cnt[(uint64_t)t * B + j] = run;
+        run += c;
+      }
+    parallel_chunks(n, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+      uint64_t* c = cnt.data() + (uint64_t)t * B;
+      for (uint64_t i = lo; i < hi; ++i)
+        if (keep(i)) order[c[bmax - blocks_for(len[i])]++] = (uint32_t)i;
+    });
+    return run;
   }
   uint64_t m = 0;
   for (uint64_t i = 0; i < n; ++i)
@@ -168,6 +215,11 @@ bool all_equal_blocks(const uint64_t* len, uint64_t n) {
 }
 
 void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
+  if (k == 1) {
+    bounds[0] = 0;
+    bounds[1] = n;
+    return;
+  }
   uint64_t total = 0;
   for (uint64_t i = 0; i < n; ++i) total += blocks_for(len[i]);
   bounds[0] = 0;
@@ -187,10 +239,7 @@ struct Plan {
   uint64_t m = 0;
   bool ordered = false;
   std::vector<uint32_t> perm;       // sorted lane -> shard-local message
-  std::vector<uint64_t> place;      // placement -> shard-local message whose bytes it holds
-  std::vector<uint64_t> ppos;       // placement -> device arena offset (size +1)
   std::vector<uint64_t> lane_cut;   // chunk boundaries in sorted lanes
-  std::vector<uint64_t> place_cut;  // chunk boundaries in placements
   size_t next = 0;                  // next chunk to issue
   uint64_t launched = 0;            // lanes [0, launched) have a kernel enqueued
   uint64_t lanes = 0;               // messages that get a lane (one per distinct payload)
@@ -210,7 +259,7 @@ struct msha_ctx {
   // host planning buffers reused across calls
   std::vector<Plan> plans;
   std::vector<uint64_t> uid, placed;
-  std::vector<uint64_t> alias_table;
+  std::vector<uint64_t> alias_table, alias_hash;
 };
 
 namespace {
@@ -242,7 +291,7 @@ int guarded(msha_ctx* ctx, F&& f) {
 template <class F>
 void parallel_ranges(uint64_t n, uint64_t bytes, F&& f) {
   unsigned hw = std::thread::hardware_concurrency();
-  unsigned t = (unsigned)std::min<uint64_t>({(uint64_t)std::max(1u, std::min(8u, hw / 2)),
+  unsigned t = (unsigned)std::min<uint64_t>({(uint64_t)std::max(1u, std::min(16u, hw)),
                                              bytes / (4u << 20) + 1, n});
   if (t <= 1) {
     f(0, n);
@@ -272,23 +321,29 @@ bool is_pinned_host(const void* p) {
 // into T regions by the key hash's top bits and each region is built by its
 // own thread scanning the keys in index order, so "first" is preserved.
 void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vector<uint64_t>& uid,
-                std::vector<uint64_t>& table) {
+                std::vector<uint64_t>& table, std::vector<uint64_t>& hash) {
   uid.resize(n);
-  const unsigned T = n >= (1u << 20) ? 8 : 1;
+  hash.resize(n);
+  const unsigned T = n >= (1u << 20) ? 8 : 1;  // regions = build threads (power of two)
   const unsigned tbits = T == 8 ? 3 : 0;
   uint64_t cap = 1;  // per region
   while (cap * T < 2 * n) cap <<= 1;
-  table.assign(cap * T, 0);  // 0 = empty
-  auto key_hash = [&](uint64_t i) {  // splitmix64 finalizer over both fields
-    uint64_t h = off[i] ^ (len[i] * 0x9E3779B97F4A7C15ull);
-    h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
-    h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
-    return h ^ (h >> 31);
-  };
+  table.resize(cap * T);
+  // pass 1 (threaded over index chunks): one hash per key
+  parallel_chunks(n, plan_threads(n), [&](unsigned, uint64_t a, uint64_t b) {
+    for (uint64_t i = a; i < b; ++i) {  // splitmix64 finalizer over both fields
+      uint64_t h = off[i] ^ (len[i] * 0x9E3779B97F4A7C15ull);
+      h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
+      h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
+      hash[i] = h ^ (h >> 31);
+    }
+  });
+  // pass 2 (one thread per region): clear the region, insert its keys in index order
   auto build = [&](unsigned t) {
     uint64_t* reg = table.data() + (uint64_t)t * cap;
+    std::memset(reg, 0, cap * sizeof(uint64_t));  // 0 = empty
     for (uint64_t i = 0; i < n; ++i) {
-      const uint64_t h = key_hash(i);
+      const uint64_t h = hash[i];
       if (tbits && (h >> (64 - tbits)) != t) continue;
       const uint64_t tag = h & 0xffffffff00000000ull;
       for (uint64_t p = h & (cap - 1);; p = (p + 1) & (cap - 1)) {
@@ -377,11 +432,18 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     P.lanes = P.m;
     if (uid && k == 1) {  // one shard: uid[i] (the first index with i's payload) is the lane's message
       P.rep.resize(P.m);
+      const unsigned T = plan_threads(P.m);
+      std::vector<uint64_t> nl(T, 0);
+      parallel_chunks(P.m, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+        uint64_t c = 0;
+        for (uint64_t i = lo; i < hi; ++i) {
+          P.rep[i] = (uint32_t)uid[i];
+          c += uid[i] == i;
+        }
+        nl[t] = c;
+      });
       P.lanes = 0;
-      for (uint64_t i = 0; i < P.m; ++i) {
-        P.rep[i] = (uint32_t)uid[i];
-        P.lanes += uid[i] == i;
-      }
+      for (uint64_t c : nl) P.lanes += c;
       if (P.lanes == P.m) P.rep.clear();
     } else if (uid) {
       P.rep.resize(P.m);
@@ -401,6 +463,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       touched.clear();
       if (P.lanes == P.m) P.rep.clear();
     }
+    trace("representatives", t0);
     P.perm.resize(P.lanes);
     if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
       order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp, P.rep.data());
@@ -410,6 +473,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       if (P.ordered) order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp);
       else for (uint64_t i = 0; i < P.m; ++i) P.perm[i] = (uint32_t)i;
     }
+    trace("lane order", t0);
     d.use_order = P.ordered;
     d.h_meta.ensure(16 * P.m + 4 * P.m);
     uint64_t* h_off = d.h_meta.as<uint64_t>();
@@ -419,48 +483,74 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     // reads bytes uploaded by the end of chunk c.
     uint64_t acc = 0;
     if (direct) {  // the shard's span of the caller's pinned arena, uploaded as is
-      uint64_t lo = UINT64_MAX, hi = 0;
-      for (uint64_t q = 0; q < P.lanes; ++q) {
-        const uint32_t i = P.perm[q];
-        lo = std::min(lo, direct->off[d.lo + i]);
-        hi = std::max(hi, direct->off[d.lo + i] + L[i]);
-      }
-      for (uint64_t q = 0; q < P.lanes; ++q) {
-        const uint32_t i = P.perm[q];
-        h_off[q] = direct->off[d.lo + i] - lo;
-        h_len[q] = L[i];
-      }
+      const unsigned T = plan_threads(P.lanes);
+      std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
+      parallel_chunks(P.lanes, T, [&](unsigned t, uint64_t a, uint64_t b) {
+        uint64_t l = UINT64_MAX, h = 0;  // thread-local: no false sharing on tlo/thi
+        for (uint64_t q = a; q < b; ++q) {
+          const uint32_t i = P.perm[q];
+          l = std::min(l, direct->off[d.lo + i]);
+          h = std::max(h, direct->off[d.lo + i] + L[i]);
+        }
+        tlo[t] = l;
+        thi[t] = h;
+      });
+      const uint64_t lo = *std::min_element(tlo.begin(), tlo.end());
+      const uint64_t hi = *std::max_element(thi.begin(), thi.end());
+      parallel_chunks(P.lanes, T, [&](unsigned, uint64_t a, uint64_t b) {
+        for (uint64_t q = a; q < b; ++q) {
+          const uint32_t i = P.perm[q];
+          h_off[q] = direct->off[d.lo + i] - lo;
+          h_len[q] = L[i];
+        }
+      });
       d.direct_lo = lo;
       acc = hi - lo;
-      P.place.clear();
-      P.ppos.assign({0, acc});
       P.lane_cut.assign({0, P.lanes});
     } else {
-      P.place.assign(P.perm.begin(), P.perm.begin() + P.lanes);
-      P.ppos.resize(P.lanes);
-      P.lane_cut.assign(1, 0);
-      uint64_t chunk_start = 0;
-      for (uint64_t q = 0; q < P.lanes; ++q) {  // lane-indexed metadata: sequential writes
-        const uint32_t i = P.perm[q];
-        P.ppos[q] = acc;
-        h_off[q] = acc;
-        h_len[q] = L[i];
-        acc += round16(L[i]);
-        if (acc - chunk_start >= kChunkBytes && q + 1 < P.lanes) {
-          P.lane_cut.push_back(q + 1);
-          chunk_start = acc;
+      // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
+      // (lane q's payload lands at h_off[q]; payloads are placed in lane order)
+      const unsigned T = plan_threads(P.lanes);
+      std::vector<uint64_t> part(T + 1, 0);
+      parallel_chunks(P.lanes, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+        uint64_t a = 0;
+        for (uint64_t q = lo; q < hi; ++q) {
+          const uint64_t l = L[P.perm[q]];
+          h_len[q] = l;
+          a += round16(l);
         }
+        part[t + 1] = a;
+      });
+      for (unsigned t = 0; t < T; ++t) part[t + 1] += part[t];
+      parallel_chunks(P.lanes, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+        uint64_t a = part[t];
+        for (uint64_t q = lo; q < hi; ++q) {
+          h_off[q] = a;
+          a += round16(h_len[q]);
+        }
+      });
+      acc = part[T];
+      // greedy chunks of >= kChunkBytes: cut after the first lane whose end
+      // reaches the chunk's start + kChunkBytes (binary search on the scan)
+      P.lane_cut.assign(1, 0);
+      for (uint64_t q0 = 0;;) {
+        const uint64_t target = h_off[q0] + kChunkBytes;
+        const uint64_t r = (uint64_t)(std::lower_bound(h_off + q0 + 1, h_off + P.lanes, target) - h_off);
+        if (r >= P.lanes) break;  // the rest (ending at acc) is the last chunk
+        P.lane_cut.push_back(r);
+        q0 = r;
       }
-      P.ppos.push_back(acc);
       P.lane_cut.push_back(P.lanes);
     }
-    P.place_cut = P.lane_cut;
     d.arena_bytes = acc;
+    trace("placement", t0);
     if (P.ordered) std::memcpy(h_len + P.m, P.perm.data(), 4 * P.lanes);
     if (!direct) {
       uint64_t slot_bytes = 0;
-      for (size_t c = 0; c + 1 < P.place_cut.size(); ++c)
-        slot_bytes = std::max(slot_bytes, P.ppos[P.place_cut[c + 1]] - P.ppos[P.place_cut[c]]);
+      for (size_t c = 0; c + 1 < P.lane_cut.size(); ++c) {
+        const uint64_t e = P.lane_cut[c + 1] < P.lanes ? h_off[P.lane_cut[c + 1]] : acc;
+        slot_bytes = std::max(slot_bytes, e - h_off[P.lane_cut[c]]);
+      }
       d.slot[0].ensure(std::max<uint64_t>(slot_bytes, 16));
       d.slot[1].ensure(std::max<uint64_t>(slot_bytes, 16));
     }
@@ -481,6 +571,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     HIPCHK(hipEventRecord(d.slot_free[1], d.copy_stream));
   }
   const double t_plan = now_ms();
+  trace("planned (metadata H2D queued)", t0);
   // Issue chunks round-robin over the GPUs so every copy engine stays busy.
   for (bool more = true; more;) {
     more = false;
@@ -491,8 +582,10 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       more = true;
       const size_t c = P.next++;
       const uint64_t q1 = P.lane_cut[c + 1];
-      const uint64_t u0 = P.place_cut[c], u1 = P.place_cut[c + 1];
-      const uint64_t b0 = direct ? 0 : P.ppos[u0], b1 = direct ? d.arena_bytes : P.ppos[u1];
+      const uint64_t u0 = P.lane_cut[c], u1 = P.lane_cut[c + 1];
+      const uint64_t* h_off = d.h_meta.as<uint64_t>();  // lane -> arena offset (gather mode)
+      const uint64_t b0 = direct ? 0 : h_off[u0];
+      const uint64_t b1 = direct || u1 >= P.lanes ? d.arena_bytes : h_off[u1];
       PinBuf& slot = d.slot[c & 1];
       HIPCHK(hipSetDevice(d.id));
       if (direct) {
@@ -504,7 +597,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
         const double g0 = now_ms();
         uint8_t* dst = slot.as<uint8_t>();
         parallel_ranges(u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
-          for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.place[u], dst + (P.ppos[u] - b0));
+          for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.perm[u], dst + (h_off[u] - b0));
         });
         gather_ms += now_ms() - g0;
         if (b1 > b0)
@@ -557,12 +650,13 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
     if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
     const std::vector<uint32_t>& rep = plans[s].rep;
-    if (rep.empty()) {
-      std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
-    } else {
-      const uint8_t* h = d.h_out.as<uint8_t>();
-      for (uint64_t i = 0; i < m; ++i) std::memcpy(out + 32 * (d.lo + i), h + 32 * (uint64_t)rep[i], 32);
-    }
+    const uint8_t* h = d.h_out.as<uint8_t>();
+    parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
+      if (rep.empty())
+        std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));
+      else
+        for (uint64_t i = a; i < b; ++i) std::memcpy(out + 32 * (d.lo + i), h + 32 * (uint64_t)rep[i], 32);
+    });
   }
   ctx->stats.calls++;
   ctx->stats.plan_ms = t_plan - t0;
@@ -688,23 +782,46 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
   if (n >= 0xffffffffull) return fail(ctx, MSHA_ERR_INVALID_ARG, "more than 2^32-2 messages in one call");
   const double t0 = now_ms();
   return guarded(ctx, [&] {
-    // One pass: bounds, the covered span, total bytes and blocks.
+    // One pass (threaded for large batches): bounds, the covered span, total
+    // bytes and blocks, and the OR of all offsets (alignment).
+    struct Acc {
+      uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0, offbits = 0, bad = UINT64_MAX;
+    };
+    const unsigned T = plan_threads(n);
+    std::vector<Acc> acc(T);
+    parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
+      Acc r;
+      for (uint64_t i = a; i < b; ++i) {
+        if (len[i] > arena_len || off[i] > arena_len - len[i]) {
+          r.bad = i;
+          break;
+        }
+        r.offbits |= off[i];
+        r.lo = std::min(r.lo, off[i]);
+        r.hi = std::max(r.hi, off[i] + len[i]);
+        r.sum += len[i];
+        r.blocks += blocks_for(len[i]);
+      }
+      acc[t] = r;
+    });
     uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0, offbits = reinterpret_cast<uintptr_t>(arena);
-    for (uint64_t i = 0; i < n; ++i) {
-      if (len[i] > arena_len || off[i] > arena_len - len[i])
-        throw MshaError(MSHA_ERR_INVALID_ARG, "message " + std::to_string(i) + " [off+len] outside arena");
-      offbits |= off[i];
-      lo = std::min(lo, off[i]);
-      hi = std::max(hi, off[i] + len[i]);
-      sum += len[i];
-      blocks += blocks_for(len[i]);
+    for (const Acc& r : acc) {  // chunks in index order: the first bad message is reported
+      if (r.bad != UINT64_MAX)
+        throw MshaError(MSHA_ERR_INVALID_ARG, "message " + std::to_string(r.bad) + " [off+len] outside arena");
+      lo = std::min(lo, r.lo);
+      hi = std::max(hi, r.hi);
+      sum += r.sum;
+      blocks += r.blocks;
+      offbits |= r.offbits;
     }
     const bool aligned16 = (offbits & 15) == 0;
     // Overlapping payloads (sum of lengths > the span they cover) means there
     // may be aliases: give every message the index of the first message with
     // the same (off, len).
     const bool aliases = n > 1 && sum > hi - lo;
-    if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table);
+    trace("validated", t0);
+    if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table, ctx->alias_hash);
+    trace("aliases", t0);
     // Zero-copy upload when the caller packed into pinned memory (msha_pinned_alloc)
     // with 16-byte aligned message starts and little waste between messages.
     Direct dir{arena, off};

@@ -92,3 +92,16 @@ def test_order_by_blocks_is_descending_stable_permutation():
         idx = o[b == v]
         assert np.all(np.diff(idx.astype(np.int64)) > 0)
     assert order_by_blocks(np.zeros(0, dtype=np.uint64)).size == 0
+
+
+@pytest.mark.parametrize("n,maxlen", [(300_000, 5000), (300_000, 1 << 23), (70_000, 1 << 27)])
+def test_order_by_blocks_threaded_matches_stable_argsort(n, maxlen):
+    """Large batches take the threaded counting sort (per-thread histograms), or the
+    single-thread/radix paths for huge block counts: all equal a stable argsort."""
+    from mirbft_amd.engine import order_by_blocks
+    rng = np.random.default_rng(n ^ maxlen)
+    lens = rng.integers(0, maxlen, n).astype(np.uint64)
+    lens[::7] = 512                     # many ties
+    blocks = (lens >> 6) + np.where((lens & 63) < 56, 1, 2)
+    exp = np.argsort(-blocks.astype(np.int64), kind="stable")
+    assert np.array_equal(order_by_blocks(lens).astype(np.int64), exp)

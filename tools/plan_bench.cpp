@@ -43,9 +43,9 @@ int main(int argc, char** argv) {
   }
   t = T("validate+span+blocks", t);
   std::vector<uint64_t> uid;
-  std::vector<uint64_t> table;
+  std::vector<uint64_t> table, hashes;
   for (int rep_i = 0; rep_i < 2; ++rep_i) {  // second round: buffers warm (as in a context)
-    alias_uids(off.data(), len.data(), n, uid, table);
+    alias_uids(off.data(), len.data(), n, uid, table, hashes);
     t = T("alias_uids", t);
   }
   std::vector<uint32_t> rep(n);
