@@ -12,6 +12,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <functional>
+#include <condition_variable>
 #include <exception>
 #include <new>
 #include <stdexcept>
@@ -132,16 +135,98 @@ inline unsigned plan_threads(uint64_t n) {
   const unsigned hw = std::thread::hardware_concurrency();
   return std::max(1u, std::min(16u, hw));
 }
+// Process-wide worker pool for those phases (thread creation would otherwise
+// cost ~0.1 ms per thread per phase). run(T, job) calls job(t) for t in [0, T)
+// on the workers and the calling thread, and returns when all are done. One
+// run at a time: a caller that finds the pool busy (another context planning
+// concurrently) runs its tasks on fresh threads instead.
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool pool;
+    return pool;
+  }
+  void run(unsigned T, const std::function<void(unsigned)>& job) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock() || workers_.empty()) {
+      std::vector<std::thread> th;
+      for (unsigned t = 1; t < T; ++t) th.emplace_back(job, t);
+      job(0);
+      for (auto& x : th) x.join();
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &job;
+      ntasks_ = T;
+      next_ = 0;
+      pending_ = T;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& w : workers_) w.join();
+  }
+
+ private:
+  WorkerPool() {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    for (unsigned i = 1; i < std::min(16u, hw); ++i) workers_.emplace_back([this] { loop(); });
+  }
+  void work() {  // claim and run tasks of the current generation
+    for (;;) {
+      unsigned t;
+      const std::function<void(unsigned)>* job;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!job_ || next_ >= ntasks_) return;
+        t = next_++;
+        job = job_;
+      }
+      (*job)(t);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  unsigned ntasks_ = 0, next_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 template <class F>
 void parallel_chunks(uint64_t n, unsigned T, F&& f) {
   if (T <= 1) {
     f(0u, (uint64_t)0, n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(T);
-  for (unsigned t = 0; t < T; ++t) th.emplace_back([&, t] { f(t, n * t / T, n * (t + 1) / T); });
-  for (auto& x : th) x.join();
+  const std::function<void(unsigned)> job = [&](unsigned t) { f(t, n * t / T, n * (t + 1) / T); };
+  WorkerPool::get().run(T, job);
 }
 
 // Descending-block-count permutation so every wavefront gets messages of equal
@@ -297,11 +382,8 @@ void parallel_ranges(uint64_t n, uint64_t bytes, F&& f) {
     f(0, n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(t);
-  for (unsigned k = 0; k < t; ++k)
-    th.emplace_back([&, k] { f(n * k / t, n * (k + 1) / t); });
-  for (auto& x : th) x.join();
+  const std::function<void(unsigned)> job = [&](unsigned k) { f(n * k / t, n * (k + 1) / t); };
+  WorkerPool::get().run(t, job);
 }
 
 // Is p inside page-locked host memory the GPU can DMA from (hipHostMalloc /
@@ -365,9 +447,8 @@ void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vecto
     build(0);
     return;
   }
-  std::vector<std::thread> th;
-  for (unsigned t = 0; t < T; ++t) th.emplace_back(build, t);
-  for (auto& x : th) x.join();
+  const std::function<void(unsigned)> job = [&](unsigned t) { build(t); };
+  WorkerPool::get().run(T, job);
 }
 
 // Host-memory execution of one batch (the body of every host entry point):
