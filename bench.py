@@ -135,8 +135,9 @@ def cpu_baseline(w, seconds: float):
         line["openssl"] = {"cpu": cpu, "sha_ni": sha_ni,
                            "1_thread": {"value": v1, "gbps": g1},
                            f"{CPU_THREADS}_threads": {"value": vt, "gbps": gt},
-                           "source": "oracle/sha256_openssl.c (EVP_Digest), stronger than the reference's "
-                                     "Go 1.15/1.16 crypto/sha256 (no SHA-NI path)"}
+                           "source": "oracle/sha256_openssl.c (EVP_Digest*): the fastest CPU SHA-256 on this "
+                                     "host (SHA-NI), a strong stand-in for the reference's Go crypto/sha256, "
+                                     "which cannot be built here"}
     except (OSError, RuntimeError) as e:   # libcrypto missing: report the port only
         line["openssl"] = {"error": str(e)}
     return line

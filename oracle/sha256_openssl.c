@@ -4,8 +4,8 @@
  * for one-part messages, each digest computed by OpenSSL libcrypto
  * (EVP_Digest{Init,Update,Final}, SHA-256; SHA-NI on CPUs that have it), split over
  * T POSIX threads in contiguous ranges. It cross-checks sha256_oracle.c and is
- * bench.py's strongest CPU baseline (the reference's own Go 1.15/1.16
- * crypto/sha256 cannot be built in this image and has no SHA-NI path).
+ * bench.py's strongest CPU baseline (the reference's own Go crypto/sha256
+ * cannot be built in this image).
  */
 #include <openssl/evp.h>
 #include <pthread.h>
