@@ -11,7 +11,11 @@ one engine launch over the whole batch. Default workload: BASELINE config c2
 quoted on). N>1: one process per GPU (torchrun), every rank hashes its own
 disjoint 2^20-request slice (weak scaling, no collective on the data path);
 the timed region is bracketed by barrier + synchronize and the max over ranks
-is taken. Rank 0 prints ONE JSON line.
+is taken. Rank 0 prints ONE JSON line. Warmup: the W steps, then more untimed
+steps until --min-warmup-ms (300) of wall time has passed -- MI355X clocks need
+~100 ms of load to settle, and a cold timed region measures the clock ramp
+(c2: 0.395 ms per launch after 3 warmup steps, 0.330 ms after 200); the line
+reports warmup_steps_run and warmup_ms.
 
 roofline: the kernel is integer-VALU bound. achieved = 1400 int32 ops per
 64-byte block (the minimal gfx950 instruction count) x blocks per
@@ -44,8 +48,12 @@ METRIC = "SHA-256 digests/sec + GB/s hashed (1/2/4/8 MI355X), % integer-ALU roof
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--steps", type=int, default=100)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--min-warmup-ms", type=float, default=300.0,
+                   help="after the W warmup steps, keep running untimed steps until this much "
+                        "wall time has passed: MI355X clocks take ~100 ms of load to settle, "
+                        "and a timed region that starts cold measures the ramp, not the kernel")
     p.add_argument("--config", default="c2",
                    help="c2 (default) | c3 | c3dd (digest-of-digests form) | c4 | c5 | ub:N:SIZE (experiment: "
                         "N uniform messages via the batch kernel) | "
@@ -244,9 +252,18 @@ def main():
         def step():
             eng.digest_batch_device(d_arena, d_off, d_len, d_out, stream, order=d_order)
 
+    tw = time.perf_counter()
+    warm = 0
     for _ in range(args.warmup):
         step()
+        warm += 1
     torch.cuda.synchronize(dev)
+    while (time.perf_counter() - tw) * 1e3 < args.min_warmup_ms:
+        for _ in range(8):
+            step()
+            warm += 1
+        torch.cuda.synchronize(dev)
+    warmup_ms = (time.perf_counter() - tw) * 1e3
     eng.device_status()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -292,6 +309,8 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_steps_run": warm,
+            "warmup_ms": warmup_ms,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if args.config == "c5" else "weak",  # c5: 8M actions per node

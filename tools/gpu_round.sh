@@ -17,13 +17,13 @@ fi
 if [[ $STEPS == all || $STEPS == *bench* ]]; then
   for cfg in ${CONFIGS:-c2 c3 c3dd c4 c5}; do
     extra="--no-cpu-baseline"; [ $cfg == c2 ] && extra=""
-    timeout -k 10 400 python bench.py --config $cfg --steps ${BSTEPS:-10} $extra > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err; stop_on_fault $? bench_$cfg
+    timeout -k 10 400 python bench.py --config $cfg ${BSTEPS:+--steps $BSTEPS} $extra > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err; stop_on_fault $? bench_$cfg
     cat gpurun_out/bench_$cfg.json
   done
 fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
   rm -rf gpurun_out/prof
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --config ${PCFG:-c2} --steps 10 --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1; stop_on_fault $? rocprof
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --config ${PCFG:-c2} --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1; stop_on_fault $? rocprof
   find gpurun_out/prof -name "*kernel_stats*" | head -3
   for f in $(find gpurun_out/prof -name "*kernel_stats.csv"); do cat $f; done
 fi

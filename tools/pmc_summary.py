@@ -8,7 +8,8 @@ profiles/r01_traffic.json + WRITE_SIZE).
 
     python3 tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc.json
 
-Dispatch 1 of each run is the bench's warmup launch and is skipped.
+Only the last 3 dispatches of each run (bench.py's timed steps) are used; the
+earlier ones are warmup (the bench warms up for >= 300 ms so clocks settle).
 """
 import csv
 import json
@@ -46,8 +47,11 @@ def counters(run):
     return vals, dur
 
 
+TIMED = 3  # bench.py --steps 3 in tools/pmc_valu.sh: the last 3 dispatches are the timed ones
+
+
 def mean_timed(vals, dur, name):
-    ds = sorted(vals)[1:] or sorted(vals)
+    ds = sorted(vals)[-TIMED:]   # everything before them is warmup (clocks settling)
     return sum(vals[d].get(name, 0.0) for d in ds) / len(ds), sum(dur[d] for d in ds) / len(ds)
 
 

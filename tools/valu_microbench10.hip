@@ -4,6 +4,9 @@
 // waves of a SIMD (from 8 different workgroups) drift apart. Here the waves of
 // one workgroup (512 or 1024 threads: 2 or 4 per SIMD) re-align with
 // s_barrier every R rounds, on register-resident data (part 4's harness).
+// Every variant is timed after >= 500 ms of warm load (settled clocks); the
+// 256-thread, no-barrier row is the production form's ceiling (bench.py's
+// ISA_MIX_CEILING_TOPS).
 // Build: hipcc --offload-arch=gfx950 -O3 -I mirbft_amd/csrc -o tools/valu_microbench10 tools/valu_microbench10.hip
 #include <hip/hip_runtime.h>
 #include <cstdio>
@@ -72,7 +75,16 @@ int main() {
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
   auto timeit = [&](auto launch) {
-    launch();
+    // clocks settle after ~100 ms of load: keep the GPU busy for >= 500 ms first
+    hipEvent_t w0, w1;
+    CHECK(hipEventCreate(&w0)); CHECK(hipEventCreate(&w1));
+    CHECK(hipEventRecord(w0));
+    for (float el = 0; el < 500.f;) {
+      for (int i = 0; i < 20; ++i) launch();
+      CHECK(hipEventRecord(w1));
+      CHECK(hipEventSynchronize(w1));
+      CHECK(hipEventElapsedTime(&el, w0, w1));
+    }
     CHECK(hipDeviceSynchronize());
     float best = 1e30f;
     for (int r = 0; r < 7; ++r) {
