@@ -151,17 +151,23 @@ def cpu_baseline(w, seconds: float):
     return line
 
 
-TRAFFIC_FILE = "profiles/r01_traffic.json"
+PMC_FILE = "profiles/r01_pmc.json"          # tools/pmc_valu.sh -> tools/pmc_summary.py
+TRAFFIC_FILE = "profiles/r01_traffic.json"  # tools/pmc_traffic.sh (first collection)
 
 
 def measured_traffic(cfg: str):
-    """HBM bytes per launch from the committed PMC profile (tools/pmc_traffic.sh ->
-    tools/traffic_summary.py); None when this config was not profiled."""
+    """HBM bytes per launch from the committed PMC profiles (FETCH_SIZE x the gfx950
+    calibration + WRITE_SIZE, separate rocprofv3 passes); (bytes, source) or (None, None)."""
+    try:
+        with open(os.path.join(ROOT, PMC_FILE)) as f:
+            return json.load(f)["configs"][f"{cfg}_auto"]["hbm_bytes"], PMC_FILE
+    except (OSError, KeyError, ValueError):
+        pass
     try:
         with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
-            return json.load(f)["configs"][cfg]["traffic_bytes_per_launch"]
+            return json.load(f)["configs"][cfg]["traffic_bytes_per_launch"], TRAFFIC_FILE
     except (OSError, KeyError, ValueError):
-        return None
+        return None, None
 
 
 def verify_sample(w, d_out, k: int = 512) -> None:
@@ -324,14 +330,14 @@ def main():
             "kernel_ms_mean": kern_ms,
             "roofline": {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS,
                          "unit": "Tint32op/s", "frac": achieved / PEAK_VALU_TOPS,
-                         "traffic": measured_traffic(args.config),
-                         "traffic_source": TRAFFIC_FILE if measured_traffic(args.config) else None,
+                         "traffic": measured_traffic(args.config)[0],
+                         "traffic_source": measured_traffic(args.config)[1],
                          "ops_per_block": OPS_PER_BLOCK,
                          "note": "peak = full-rate int32 VALU (VOP2/v_bitop3, 2 cycles per wave64 "
-                                 "instr at 2.4 GHz); SHA-256's mix is 64% half-rate ops (v_alignbit, "
-                                 "v_add3) and costs ~4 SIMD cycles per instruction on gfx950, so the "
-                                 "ISA-mix ceiling measured on a register-resident loop is ~0.50 of "
-                                 "this peak (DESIGN.md, profiles/r01_valu_microbench*)",
+                                 "instr at 2.4 GHz); SHA-256's mix is ~60% half-rate ops (v_alignbit, "
+                                 "v_add3) and costs ~3.9-4.1 SIMD cycles per instruction on gfx950, so "
+                                 "the ISA-mix ceiling measured on a register-resident loop is ~0.50 of "
+                                 "this peak (DESIGN.md, profiles/r01_valu_microbench*, r01_pmc.json)",
                          "algorithmic_bytes_per_launch": w.message_bytes + 32 * w.n + 16 * w.n,
                          "isa_mix_ceiling": ISA_MIX_CEILING_TOPS,
                          "frac_of_isa_mix_ceiling": achieved / ISA_MIX_CEILING_TOPS},
