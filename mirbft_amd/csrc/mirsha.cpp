@@ -344,7 +344,8 @@ struct msha_ctx {
   // host planning buffers reused across calls
   std::vector<Plan> plans;
   std::vector<uint64_t> uid, placed;
-  std::vector<uint64_t> alias_table, alias_hash;
+  std::vector<uint64_t> alias_table, alias_bucket;
+  std::vector<uint32_t> alias_tag;
 };
 
 namespace {
@@ -398,37 +399,79 @@ bool is_pinned_host(const void* p) {
 }
 
 // uid[i] = the first index j <= i with (off[j], len[j]) == (off[i], len[i]).
-// Open addressing (linear probing); an entry is (index + 1) | hash-tag << 32,
-// so a probe dereferences off/len only when the tags match. The table is split
-// into T regions by the key hash's top bits and each region is built by its
-// own thread scanning the keys in index order, so "first" is preserved.
+// Open addressing (linear probing) over R regions picked by the key hash's top
+// bits. Pass 1 hashes every key and counts keys per (index chunk, region);
+// pass 2 scatters (tag << 32 | index) into per-region buckets, in index order;
+// pass 3 builds each region's table on its own worker from its bucket alone,
+// prefetching the slot of the key kPrefetch ahead (the probes are the cost:
+// random accesses into a table far larger than the caches). A table entry is
+// (tag << 32) | (index + 1); off/len are dereferenced only on a tag match, and
+// "first" is preserved because a region inserts its keys in index order.
 void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vector<uint64_t>& uid,
-                std::vector<uint64_t>& table, std::vector<uint64_t>& hash) {
+                std::vector<uint64_t>& table, std::vector<uint64_t>& bucket, std::vector<uint32_t>& tagv) {
   uid.resize(n);
-  hash.resize(n);
-  const unsigned T = n >= (1u << 20) ? 8 : 1;  // regions = build threads (power of two)
-  const unsigned tbits = T == 8 ? 3 : 0;
-  uint64_t cap = 1;  // per region
-  while (cap * T < 2 * n) cap <<= 1;
-  table.resize(cap * T);
-  // pass 1 (threaded over index chunks): one hash per key
-  parallel_chunks(n, plan_threads(n), [&](unsigned, uint64_t a, uint64_t b) {
-    for (uint64_t i = a; i < b; ++i) {  // splitmix64 finalizer over both fields
+  bucket.resize(n);
+  tagv.resize(n);
+  const unsigned rbits = n >= (1u << 20) ? 4 : 0;
+  const unsigned R = 1u << rbits;  // regions (one pass-3 task each)
+  const unsigned T = plan_threads(n);
+  std::vector<uint64_t> cnt((size_t)T * R, 0);
+  // pass 1: one hash per key (splitmix64 finalizer over both fields) -> its 32-bit tag
+  parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t* c = cnt.data() + (size_t)t * R;
+    for (uint64_t i = a; i < b; ++i) {
       uint64_t h = off[i] ^ (len[i] * 0x9E3779B97F4A7C15ull);
       h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
       h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
-      hash[i] = h ^ (h >> 31);
+      const uint32_t tag = (uint32_t)((h ^ (h >> 31)) >> 32);
+      tagv[i] = tag;
+      ++c[rbits ? tag >> (32 - rbits) : 0];
     }
   });
-  // pass 2 (one thread per region): clear the region, insert its keys in index order
-  auto build = [&](unsigned t) {
-    uint64_t* reg = table.data() + (uint64_t)t * cap;
-    std::memset(reg, 0, cap * sizeof(uint64_t));  // 0 = empty
-    for (uint64_t i = 0; i < n; ++i) {
-      const uint64_t h = hash[i];
-      if (tbits && (h >> (64 - tbits)) != t) continue;
-      const uint64_t tag = h & 0xffffffff00000000ull;
-      for (uint64_t p = h & (cap - 1);; p = (p + 1) & (cap - 1)) {
+  // bucket layout: region-major, chunk order inside a region (= index order)
+  std::vector<uint64_t> rstart(R + 1, 0), base((size_t)T * R);
+  {
+    uint64_t acc = 0;
+    for (unsigned r = 0; r < R; ++r) {
+      rstart[r] = acc;
+      for (unsigned t = 0; t < T; ++t) {
+        base[(size_t)t * R + r] = acc;
+        acc += cnt[(size_t)t * R + r];
+      }
+    }
+    rstart[R] = acc;
+  }
+  // pass 2: scatter
+  parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t* w = base.data() + (size_t)t * R;
+    for (uint64_t i = a; i < b; ++i) {
+      const uint32_t tag = tagv[i];
+      bucket[w[rbits ? tag >> (32 - rbits) : 0]++] = (uint64_t)tag << 32 | i;
+    }
+  });
+  // per-region table capacity: a power of two >= 2x its keys
+  std::vector<uint64_t> cap(R), tstart(R + 1, 0);
+  for (unsigned r = 0; r < R; ++r) {
+    uint64_t c = 16;
+    while (c < 2 * (rstart[r + 1] - rstart[r])) c <<= 1;
+    cap[r] = c;
+    tstart[r + 1] = tstart[r] + c;
+  }
+  if (table.size() < tstart[R]) table.resize(tstart[R]);
+  // pass 3: one task per region
+  static const uint64_t kPrefetch = getenv("PF") ? atoi(getenv("PF")) : 16;
+  const std::function<void(unsigned)> build = [&](unsigned r) {
+    uint64_t* reg = table.data() + tstart[r];
+    const uint64_t mask = cap[r] - 1;
+    std::memset(reg, 0, cap[r] * sizeof(uint64_t));  // 0 = empty
+    const uint64_t* bk = bucket.data() + rstart[r];
+    const uint64_t m = rstart[r + 1] - rstart[r];
+    for (uint64_t k = 0; k < m; ++k) {
+      const uint64_t ahead = k + kPrefetch < m ? bk[k + kPrefetch] : bk[k];
+      __builtin_prefetch(reg + ((ahead >> 32) & mask), 1);
+      const uint64_t e0 = bk[k];
+      const uint64_t i = e0 & 0xffffffffull, tag = e0 & 0xffffffff00000000ull;
+      for (uint64_t p = (e0 >> 32) & mask;; p = (p + 1) & mask) {
         const uint64_t e = reg[p];
         if (e == 0) {
           reg[p] = tag | (i + 1);
@@ -443,12 +486,8 @@ void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vecto
       }
     }
   };
-  if (T == 1) {
-    build(0);
-    return;
-  }
-  const std::function<void(unsigned)> job = [&](unsigned t) { build(t); };
-  WorkerPool::get().run(T, job);
+  if (R == 1) build(0);
+  else WorkerPool::get().run(R, build);
 }
 
 // Host-memory execution of one batch (the body of every host entry point):
@@ -476,14 +515,55 @@ constexpr uint64_t kChunkBytes = 32ull << 20;
 struct Direct {
   const uint8_t* arena;
   const uint64_t* off;
+  bool uploaded = false;  // upload_direct_spans() already queued every shard's span
 };
+
+// Direct mode: queue each shard's byte span of the caller's pinned arena for DMA
+// (copy stream) BEFORE the lanes are planned, so PCIe runs while the host builds
+// the alias table, lane order and metadata: a large batch's planning takes about
+// as long as its upload (c5: ~55 ms of planning beside ~65 ms of H2D). The span
+// of a shard is order-independent (min off .. max off+len over its messages),
+// so it is known as soon as the batch is partitioned. bounds: k+1 entries.
+void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off,
+                         const uint64_t* len, const uint8_t* arena, uint64_t* bounds) {
+  const uint32_t k = (uint32_t)ctx->devs.size();
+  partition(len, n, k, bounds);
+  for (uint32_t s = 0; s < k; ++s) {
+    Device& d = ctx->devs[s];
+    const uint64_t a = bounds[s], b = bounds[s + 1];
+    if (a == b) continue;
+    const unsigned T = plan_threads(b - a);
+    std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
+    parallel_chunks(b - a, T, [&](unsigned t, uint64_t x, uint64_t y) {
+      uint64_t l = UINT64_MAX, h = 0;  // thread-local: no false sharing on tlo/thi
+      for (uint64_t i = a + x; i < a + y; ++i) {
+        l = std::min(l, off[i]);
+        h = std::max(h, off[i] + len[i]);
+      }
+      tlo[t] = l;
+      thi[t] = h;
+    });
+    const uint64_t lo = *std::min_element(tlo.begin(), tlo.end());
+    const uint64_t hi = *std::max_element(thi.begin(), thi.end());
+    d.direct_lo = lo;
+    d.arena_bytes = hi - lo;
+    HIPCHK(hipSetDevice(d.id));
+    d.arena.ensure(d.arena_bytes + msha::kArenaSlack);
+    if (hi > lo)
+      HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>(), arena + lo, hi - lo, hipMemcpyHostToDevice,
+                            d.copy_stream));
+  }
+  trace("direct spans queued", t0);
+}
 
 template <class Gather>
 void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, const uint64_t* uid,
-                  uint8_t* out, Gather&& gather, const Direct* direct = nullptr) {
+                  uint8_t* out, Gather&& gather, const Direct* direct = nullptr,
+                  const uint64_t* pre_bounds = nullptr) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   std::vector<uint64_t> bounds(k + 1);
-  partition(len, n, k, bounds.data());
+  if (pre_bounds) std::copy(pre_bounds, pre_bounds + k + 1, bounds.begin());
+  else partition(len, n, k, bounds.data());
   double gather_ms = 0;
 
   std::vector<Plan>& plans = ctx->plans;
@@ -565,19 +645,22 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     uint64_t acc = 0;
     if (direct) {  // the shard's span of the caller's pinned arena, uploaded as is
       const unsigned T = plan_threads(P.lanes);
-      std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
-      parallel_chunks(P.lanes, T, [&](unsigned t, uint64_t a, uint64_t b) {
-        uint64_t l = UINT64_MAX, h = 0;  // thread-local: no false sharing on tlo/thi
-        for (uint64_t q = a; q < b; ++q) {
-          const uint32_t i = P.perm[q];
-          l = std::min(l, direct->off[d.lo + i]);
-          h = std::max(h, direct->off[d.lo + i] + L[i]);
-        }
-        tlo[t] = l;
-        thi[t] = h;
-      });
-      const uint64_t lo = *std::min_element(tlo.begin(), tlo.end());
-      const uint64_t hi = *std::max_element(thi.begin(), thi.end());
+      uint64_t lo = d.direct_lo, hi = d.direct_lo + d.arena_bytes;
+      if (!direct->uploaded) {
+        std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
+        parallel_chunks(P.lanes, T, [&](unsigned t, uint64_t a, uint64_t b) {
+          uint64_t l = UINT64_MAX, h = 0;  // thread-local: no false sharing on tlo/thi
+          for (uint64_t q = a; q < b; ++q) {
+            const uint32_t i = P.perm[q];
+            l = std::min(l, direct->off[d.lo + i]);
+            h = std::max(h, direct->off[d.lo + i] + L[i]);
+          }
+          tlo[t] = l;
+          thi[t] = h;
+        });
+        lo = *std::min_element(tlo.begin(), tlo.end());
+        hi = *std::max_element(thi.begin(), thi.end());
+      }
       parallel_chunks(P.lanes, T, [&](unsigned, uint64_t a, uint64_t b) {
         for (uint64_t q = a; q < b; ++q) {
           const uint32_t i = P.perm[q];
@@ -670,7 +753,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       PinBuf& slot = d.slot[c & 1];
       HIPCHK(hipSetDevice(d.id));
       if (direct) {
-        if (b1 > b0)
+        if (b1 > b0 && !direct->uploaded)
           HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>(), direct->arena + d.direct_lo, b1 - b0,
                                 hipMemcpyHostToDevice, d.copy_stream));
       } else {
@@ -901,16 +984,22 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
     // the same (off, len).
     const bool aliases = n > 1 && sum > hi - lo;
     trace("validated", t0);
-    if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table, ctx->alias_hash);
-    trace("aliases", t0);
     // Zero-copy upload when the caller packed into pinned memory (msha_pinned_alloc)
-    // with 16-byte aligned message starts and little waste between messages.
-    Direct dir{arena, off};
+    // with 16-byte aligned message starts and little waste between messages:
+    // the spans go out now, and the planning below overlaps their DMA.
     const bool direct = aligned16 && hi - lo <= std::min(sum, hi - lo) + 16 * n + (1u << 20) &&
                         is_pinned_host(arena + lo);
+    Direct dir{arena, off};
+    std::vector<uint64_t> bounds(ctx->devs.size() + 1);
+    if (direct) {
+      upload_direct_spans(ctx, t0, n, off, len, arena, bounds.data());
+      dir.uploaded = true;
+    }
+    if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table, ctx->alias_bucket, ctx->alias_tag);
+    trace("aliases", t0);
     run_pipeline(ctx, t0, n, len, aliases ? ctx->uid.data() : nullptr, out,
                  [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); },
-                 direct ? &dir : nullptr);
+                 direct ? &dir : nullptr, direct ? bounds.data() : nullptr);
     ctx->stats.direct_calls += direct;
     ctx->stats.messages += n;
     ctx->stats.message_bytes += sum;

@@ -384,3 +384,23 @@ def test_pinned_arena_direct_upload(engine):
     # pageable memory: gather path
     assert np.array_equal(engine.digest_batch(w.arena, w.off, w.len), exp)
     assert engine.stats()["direct_calls"] == before + 1
+
+
+def _oracle_dedup(w):
+    """Oracle digests of a batch with many aliases: hash each distinct (off, len) once."""
+    key = np.stack([w.off, w.len], axis=1)
+    uniq, inv = np.unique(key, axis=0, return_inverse=True)
+    return oracle.digest_batch(w.arena, uniq[:, 0].copy(), uniq[:, 1].copy())[inv.reshape(-1)]
+
+
+def test_alias_table_regions_large_batch(engine):
+    """>= 2^20 messages with aliases: the alias table is built over 16 hash regions
+    (bucketed keys, prefetched probes); pageable (gather) and pinned (direct) paths."""
+    w = W.c5_storm((1 << 20) + 4099)
+    exp = _oracle_dedup(w)
+    assert np.array_equal(engine.digest_batch(w.arena, w.off, w.len), exp)
+    pinned = engine.pinned_empty(w.arena.size)
+    pinned[:] = w.arena
+    before = engine.stats()["direct_calls"]
+    assert np.array_equal(engine.digest_batch(pinned, w.off, w.len), exp)
+    assert engine.stats()["direct_calls"] == before + 1

@@ -5,6 +5,7 @@
 #include "../mirbft_amd/csrc/mirsha.cpp"
 
 #include <cstdio>
+#include <map>
 #include <random>
 
 // The launchers live in kernels.hip; this host-only harness never launches.
@@ -43,10 +44,19 @@ int main(int argc, char** argv) {
   }
   t = T("validate+span+blocks", t);
   std::vector<uint64_t> uid;
-  std::vector<uint64_t> table, hashes;
-  for (int rep_i = 0; rep_i < 2; ++rep_i) {  // second round: buffers warm (as in a context)
-    alias_uids(off.data(), len.data(), n, uid, table, hashes);
+  std::vector<uint64_t> table, bucket;
+  std::vector<uint32_t> tags;
+  for (int rep_i = 0; rep_i < 3; ++rep_i) {  // later rounds: buffers warm (as in a context)
+    alias_uids(off.data(), len.data(), n, uid, table, bucket, tags);
     t = T("alias_uids", t);
+  }
+  {  // check against a plain map: uid[i] = first index with the same (off, len)
+    std::map<std::pair<uint64_t, uint64_t>, uint64_t> first;
+    for (uint64_t i = 0; i < n; ++i) {
+      auto it = first.emplace(std::make_pair(off[i], len[i]), i).first;
+      if (uid[i] != it->second) { std::printf("alias mismatch at %llu\n", (unsigned long long)i); return 2; }
+    }
+    t = T("(check vs std::map)", t);
   }
   std::vector<uint32_t> rep(n);
   uint64_t lanes = 0;
