@@ -184,9 +184,10 @@ def run_e2e(args, eng, w, world):
     """End-to-end host path: numpy arena in pageable host memory -> digests in host memory."""
     out = np.empty((w.n, 32), dtype=np.uint8)   # a node reuses its result buffer
     arena = w.arena
-    if args.pinned:
+    if args.pinned:   # the cgo adapter's layout: pinned packing arena and result buffer
         arena = eng.pinned_empty(w.arena.size)
         arena[:] = w.arena
+        out = eng.pinned_empty(w.n * 32).reshape(w.n, 32)
     for _ in range(max(1, args.warmup)):
         eng.digest_batch(arena, w.off, w.len, out=out)
     t0 = time.perf_counter()

@@ -102,13 +102,13 @@ struct Device {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   hipEvent_t slot_free[2] = {nullptr, nullptr};  // staging slot s may be refilled
   hipEvent_t chunk_in = nullptr;                 // last chunk's bytes are on the device
+  std::vector<hipEvent_t> span_ev;               // direct mode: span chunk c is on the device
   DevBuf arena, off, len, order, out, err, idx, begin, table;
   PinBuf h_arena, h_meta, h_out, slot[2];
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
   uint64_t direct_lo = 0;         // direct mode: first caller-arena byte uploaded
-  bool use_order = false;
   void release() {
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table}) b->release();
     for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1]}) b->release();
@@ -116,6 +116,8 @@ struct Device {
       if (*e) (void)hipEventDestroy(*e);
       *e = nullptr;
     }
+    for (hipEvent_t e : span_ev) (void)hipEventDestroy(e);
+    span_ev.clear();
     if (stream) (void)hipStreamDestroy(stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     stream = copy_stream = nullptr;
@@ -318,6 +320,11 @@ void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
   bounds[k] = n;
 }
 
+// Direct-mode uploads go out in chunks of this size, each with its own event,
+// so kernels over the lanes whose payloads have landed start while the rest of
+// the span is still crossing PCIe (and their digests come back meanwhile).
+constexpr uint64_t kDirectChunk = 64ull << 20;
+
 // Per-GPU plan of one host-memory call (kept in the context: its vectors are
 // reused call after call, so planning does not page-fault fresh memory).
 struct Plan {
@@ -329,7 +336,57 @@ struct Plan {
   uint64_t launched = 0;            // lanes [0, launched) have a kernel enqueued
   uint64_t lanes = 0;               // messages that get a lane (one per distinct payload)
   std::vector<uint32_t> rep;        // shard-local message -> its lane's message (empty: identity)
+  std::vector<uint64_t> cut_chunk;  // direct mode: span chunk lane group g waits for
+  bool identity() const { return !ordered && rep.empty(); }  // lane q hashes message q
 };
+
+// Direct mode with chunked uploads: when the lanes' payloads ascend through the
+// span (the common request batch: equal block counts, identity lane order, an
+// ascending arena), cut the lanes into groups by the span chunk that completes
+// their payload, so lane group g is hashed as soon as chunk cut_chunk[g] lands
+// and, for identity lanes, its digests come back while later chunks upload.
+void group_lanes_by_span_chunk(Plan& P, const uint64_t* h_off, const uint64_t* h_len,
+                               uint64_t span) {
+  const uint64_t chunks = std::max<uint64_t>(1, (span + kDirectChunk - 1) / kDirectChunk);
+  const uint64_t n = P.lanes;
+  auto chunk_of = [&](uint64_t q) {
+    const uint64_t end = h_off[q] + std::max<uint64_t>(h_len[q], 1) - 1;
+    return std::min<uint64_t>(end / kDirectChunk, chunks - 1);
+  };
+  if (chunks == 1 || n == 0) {
+    P.cut_chunk.assign(1, chunks - 1);
+    return;
+  }
+  const unsigned T = plan_threads(n);
+  std::vector<uint8_t> mono(T, 1);
+  parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
+    for (uint64_t q = std::max<uint64_t>(a, 1); q < b; ++q)
+      if (chunk_of(q) < chunk_of(q - 1)) { mono[t] = 0; break; }
+  });
+  if (std::find(mono.begin(), mono.end(), 0) != mono.end()) {
+    // Lanes ordered by block count run all over the span: one group, after the
+    // last chunk. (Regrouping them costs a sort of every lane on the host,
+    // ~40 ms for 8 M lanes, for a few ms of kernel overlap.)
+    P.cut_chunk.assign(1, chunks - 1);
+    return;
+  }
+  // one lane group per chunk that completes at least one payload (binary
+  // searches over the monotone chunk index)
+  P.lane_cut.assign(1, 0);
+  P.cut_chunk.clear();
+  for (uint64_t q = 0; q < n;) {
+    const uint64_t c = chunk_of(q);
+    uint64_t lo = q + 1, hi = n;  // first lane past chunk c
+    while (lo < hi) {
+      const uint64_t mid = lo + (hi - lo) / 2;
+      if (chunk_of(mid) <= c) lo = mid + 1;
+      else hi = mid;
+    }
+    P.lane_cut.push_back(lo);
+    P.cut_chunk.push_back(c);
+    q = lo;
+  }
+}
 
 }  // namespace
 
@@ -549,9 +606,19 @@ void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* o
     d.arena_bytes = hi - lo;
     HIPCHK(hipSetDevice(d.id));
     d.arena.ensure(d.arena_bytes + msha::kArenaSlack);
-    if (hi > lo)
-      HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>(), arena + lo, hi - lo, hipMemcpyHostToDevice,
-                            d.copy_stream));
+    const uint64_t chunks = std::max<uint64_t>(1, (d.arena_bytes + kDirectChunk - 1) / kDirectChunk);
+    while (d.span_ev.size() < chunks) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      d.span_ev.push_back(e);
+    }
+    for (uint64_t c = 0; c < chunks; ++c) {
+      const uint64_t a0 = c * kDirectChunk, a1 = std::min(d.arena_bytes, a0 + kDirectChunk);
+      if (a1 > a0)
+        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + a0, arena + lo + a0, a1 - a0,
+                              hipMemcpyHostToDevice, d.copy_stream));
+      HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+    }
   }
   trace("direct spans queued", t0);
 }
@@ -561,6 +628,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
                   uint8_t* out, Gather&& gather, const Direct* direct = nullptr,
                   const uint64_t* pre_bounds = nullptr) {
   const uint32_t k = (uint32_t)ctx->devs.size();
+  const bool out_pinned = is_pinned_host(out);
   std::vector<uint64_t> bounds(k + 1);
   if (pre_bounds) std::copy(pre_bounds, pre_bounds + k + 1, bounds.begin());
   else partition(len, n, k, bounds.data());
@@ -635,7 +703,6 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       else for (uint64_t i = 0; i < P.m; ++i) P.perm[i] = (uint32_t)i;
     }
     trace("lane order", t0);
-    d.use_order = P.ordered;
     d.h_meta.ensure(16 * P.m + 4 * P.m);
     uint64_t* h_off = d.h_meta.as<uint64_t>();
     uint64_t* h_len = h_off + P.m;
@@ -671,6 +738,8 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       d.direct_lo = lo;
       acc = hi - lo;
       P.lane_cut.assign({0, P.lanes});
+      P.cut_chunk.assign(1, 0);
+      if (direct->uploaded) group_lanes_by_span_chunk(P, h_off, h_len, acc);
     } else {
       // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
       // (lane q's payload lands at h_off[q]; payloads are placed in lane order)
@@ -720,6 +789,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     }
     HIPCHK(hipSetDevice(d.id));
     d.arena.ensure(acc + msha::kArenaSlack);
+    d.h_out.ensure(32 * P.m + 4);
     d.off.ensure(8 * P.m);
     d.len.ensure(8 * P.m);
     d.out.ensure(32 * P.m);
@@ -752,8 +822,11 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       const uint64_t b1 = direct || u1 >= P.lanes ? d.arena_bytes : h_off[u1];
       PinBuf& slot = d.slot[c & 1];
       HIPCHK(hipSetDevice(d.id));
-      if (direct) {
-        if (b1 > b0 && !direct->uploaded)
+      if (direct && direct->uploaded) {
+        // the span chunk completing this lane group's payloads (queued up front)
+        HIPCHK(hipStreamWaitEvent(d.stream, d.span_ev[P.cut_chunk[c]], 0));
+      } else if (direct) {
+        if (b1 > b0)
           HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>(), direct->arena + d.direct_lo, b1 - b0,
                                 hipMemcpyHostToDevice, d.copy_stream));
       } else {
@@ -768,9 +841,11 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
           HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
                                 d.copy_stream));
       }
-      HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
-      HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
-      HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
+      if (!(direct && direct->uploaded)) {
+        HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
+        HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
+        HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
+      }
       // Kernels are launched over the lanes accumulated since the last launch
       // once they fill the GPU (2 waves per SIMD) or at the last chunk: hashing
       // runs ~30x faster than PCIe delivers bytes, so a launch per 32 MiB chunk
@@ -788,6 +863,12 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
           P.ordered ? d.order.as<uint32_t>() + l0 : nullptr, lanes,
           d.out.as<uint8_t>() + (P.ordered ? 0 : 32 * l0), d.err.as<uint32_t>(), d.cus,
           ctx->kernel_policy, d.stream));
+      // Identity lanes: these digests are final, bring them back while later
+      // chunks upload and hash (into the caller's buffer itself if it is pinned).
+      if (P.identity())
+        HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * l0,
+                              d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost,
+                              d.stream));
     }
   }
   for (uint32_t s = 0; s < k; ++s) {
@@ -796,8 +877,8 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (m == 0) continue;
     HIPCHK(hipSetDevice(d.id));
     HIPCHK(hipEventRecord(d.ev1, d.stream));
-    d.h_out.ensure(32 * m + 4);
-    HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+    if (!plans[s].identity())
+      HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
     HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
   }
   double kernel_ms = 0;
@@ -815,6 +896,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
     const std::vector<uint32_t>& rep = plans[s].rep;
     const uint8_t* h = d.h_out.as<uint8_t>();
+    if (plans[s].identity() && out_pinned) continue;  // D2H'd straight into out
     parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
       if (rep.empty())
         std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));

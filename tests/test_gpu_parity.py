@@ -404,3 +404,45 @@ def test_alias_table_regions_large_batch(engine):
     before = engine.stats()["direct_calls"]
     assert np.array_equal(engine.digest_batch(pinned, w.off, w.len), exp)
     assert engine.stats()["direct_calls"] == before + 1
+
+
+@pytest.mark.parametrize("layout", ["ascending", "reversed", "mixed_aliased"])
+@pytest.mark.parametrize("pinned_out", [False, True])
+def test_pinned_direct_chunked_span(engine, layout, pinned_out):
+    """Direct uploads larger than one 64 MiB span chunk: kernels start per landed
+    chunk (lanes grouped by the chunk completing their payload) and identity-order
+    digests come back per launch, into the caller's buffer when it is pinned."""
+    if layout == "mixed_aliased":
+        w = W.c5_storm(1 << 18)
+        exp = _oracle_dedup(w)
+    else:
+        w = W.c2_requests(3 << 16)                   # 96 MiB of 512-B requests
+        if layout == "reversed":                     # lane order descends through the span
+            w.off = w.off[::-1].copy()
+            w.len = w.len[::-1].copy()
+        exp = oracle.digest_batch(w.arena, w.off, w.len)
+    pinned = engine.pinned_empty(w.arena.size)
+    pinned[:] = w.arena
+    out = engine.pinned_empty(w.n * 32).reshape(w.n, 32) if pinned_out else None
+    before = engine.stats()["direct_calls"]
+    got = engine.digest_batch(pinned, w.off, w.len, out=out)
+    assert engine.stats()["direct_calls"] == before + 1
+    assert np.array_equal(got, exp)
+
+
+def test_pinned_direct_chunked_sharded(monkeypatch):
+    """The chunked direct path over 2 virtual shards of one GPU (each shard its own span)."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", "2")
+    with Engine(1) as e:
+        w = W.c5_storm(3 << 17)
+        pinned = e.pinned_empty(w.arena.size)
+        pinned[:] = w.arena
+        out = e.pinned_empty(w.n * 32).reshape(w.n, 32)
+        assert np.array_equal(e.digest_batch(pinned, w.off, w.len, out=out), _oracle_dedup(w))
+        w2 = W.c2_requests(3 << 16)
+        p2 = e.pinned_empty(w2.arena.size)
+        p2[:] = w2.arena
+        assert np.array_equal(e.digest_batch(p2, w2.off, w2.len),
+                              oracle.digest_batch(w2.arena, w2.off, w2.len))
+        assert e.stats()["direct_calls"] == 2
