@@ -144,7 +144,8 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
                                   const uint64_t* d_begin, uint64_t n, uint8_t* d_out,
                                   void* stream);
 /* Synchronizes the context's first device and reports (then clears) any
- * device-side error flag raised by *_device calls: MSHA_OK or MSHA_ERR_ALIGNMENT. */
+ * device-side error flag raised by *_device calls: MSHA_OK, MSHA_ERR_ALIGNMENT, or
+ * MSHA_ERR_HIP if a split-chaining handoff (kernels.hip) waited over 100 ms. */
 int msha_device_status(msha_ctx* ctx);
 
 /*

@@ -18,6 +18,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "sha256_device.hpp"
@@ -142,6 +143,229 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
   const uint8_t* p = arena + off[m];
   if (check_aligned(p, out + 32 * o, err))
     hash_message<MODE>(p, len[m], out + 32 * o);
+}
+
+// ---------------------------------------------------------------------------
+// Split chaining (tail balance). One lane per message leaves a launch of
+// q*S + r wavefronts (S = SIMDs, 0 < r < S) with r SIMDs running q+1 waves
+// while the rest run q: c3's 200 K Batch digests are 3,125 waves on 1,024
+// SIMDs, so 53 SIMDs set the time at 4 waves' worth of work (VALU busy 66 %).
+// A message's chain is serial, but it can be paused: its 32-byte state saved
+// and resumed by another wavefront. The launch runs the first q*S waves as
+// usual ("main" workgroups) and hands the remaining r waves' messages to r
+// chains of S_seg segments each; segment s of a chain does blocks
+// [nb*s/S_seg, nb*(s+1)/S_seg) of its 64 messages on a wave of its own, at high
+// issue priority, then publishes the state (in the message's own digest slot)
+// and a flag; segment s+1 (another workgroup, so usually another SIMD) waits for
+// that flag. Each SIMD then carries at most ~1/S_seg of a surplus wave instead
+// of a whole one. Segment workgroups come first in the grid and a segment
+// only ever waits on a lower workgroup id (dispatched before it), so every
+// wait is on a resident or finished wave; a wait longer than 100 ms (never
+// expected) raises error bit 2 and unblocks the chain, so every wave exits.
+// ---------------------------------------------------------------------------
+constexpr uint64_t kSplitWaitTicks = 10000000;  // 100 ms of s_memrealtime (100 MHz)
+
+// Blocks [b0, b1) of the message at p (len bytes), state in/out in s.
+__device__ __forceinline__ void hash_blocks(State& s, const uint8_t* p, uint64_t len, uint32_t b0,
+                                            uint32_t b1) {
+  const uint32_t nfull = (uint32_t)(len >> 6);
+  const uint32_t r = (uint32_t)(len & 63);
+  uint32_t raw[16];
+  uint32_t w[16];
+  for (uint32_t b = b0; b < b1; ++b) {
+    if (b <= nfull) load_block16(p + 64 * (uint64_t)b, raw);
+    if (b < nfull) {
+      to_words(raw, w);
+    } else if (b == nfull) {
+      uint32_t rr = r;
+      asm volatile("" : "+v"(rr));
+      build_tail(raw, rr, len, w);
+    } else {
+      length_block(len, w);
+    }
+    compress(s, w);
+  }
+}
+
+// Message sources of the split kernel. full<MODE>(i) hashes message i start to
+// end (main workgroups); open(i, seg) locates message i for a segment wave (the
+// first segment also runs the source's checks) and blocks() runs its blocks
+// [b0, b1).
+struct ArenaSrc {  // messages arena[off[m] : off[m]+len[m]] (k_digest_batch's form)
+  const uint8_t* arena;
+  const uint64_t* off;
+  const uint64_t* len;
+  const uint32_t* order;    // lane i -> message m (may be null)
+  const uint32_t* out_idx;  // lane i -> digest slot (may be null: slot m)
+  uint32_t* err;
+  struct Msg {
+    const uint8_t* p;
+    uint64_t len;
+    uint8_t* slot;
+    uint32_t nb;
+    bool ok;
+  };
+  template <int MODE>
+  __device__ __forceinline__ void full(uint64_t i, uint8_t* out) const {
+    const uint64_t m = order ? (uint64_t)order[i] : i;
+    const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;
+    const uint8_t* p = arena + off[m];
+    if (check_aligned(p, out + 32 * o, err)) hash_message<MODE>(p, len[m], out + 32 * o);
+  }
+  __device__ __forceinline__ Msg open(uint64_t i, uint32_t seg, uint8_t* out) const {
+    Msg g;
+    const uint64_t m = order ? (uint64_t)order[i] : i;
+    const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;
+    g.p = arena + off[m];
+    g.len = len[m];
+    g.slot = out + 32 * o;
+    g.nb = (uint32_t)((g.len >> 6) + ((g.len & 63) < 56 ? 1 : 2));
+    g.ok = seg == 0 ? check_aligned(g.p, g.slot, err) : (reinterpret_cast<uintptr_t>(g.p) & 15) == 0;
+    return g;
+  }
+  __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1) const {
+    hash_blocks(st, g.p, g.len, b0, b1);
+  }
+};
+
+// Batch / VerifyBatch digests over a table of 32-byte digests
+// (k_digest_of_digests' form): block b < cnt/2 holds digests 2b and 2b+1.
+__device__ __forceinline__ void dod_pair_block(const uint4* tab, const uint32_t* idx, uint64_t k,
+                                               uint32_t (&w)[16]) {
+  const uint4* d0 = tab + 2 * (uint64_t)idx[k];
+  const uint4* d1 = tab + 2 * (uint64_t)idx[k + 1];
+  uint4 v0 = d0[0], v1 = d0[1], v2 = d1[0], v3 = d1[1];
+  w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
+  w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
+  w[8] = bswap(v2.x); w[9] = bswap(v2.y); w[10] = bswap(v2.z); w[11] = bswap(v2.w);
+  w[12] = bswap(v3.x); w[13] = bswap(v3.y); w[14] = bswap(v3.z); w[15] = bswap(v3.w);
+}
+// The final block: the odd digest left (k < cnt), 0x80, zeros, the bit length.
+__device__ __forceinline__ void dod_final_block(const uint4* tab, const uint32_t* idx, uint64_t k,
+                                                uint64_t cnt, uint32_t (&w)[16]) {
+  if (k < cnt) {  // one digest left: 32 bytes + 0x80 + zeros + length fit one block
+    const uint4* d0 = tab + 2 * (uint64_t)idx[k];
+    uint4 v0 = d0[0], v1 = d0[1];
+    w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
+    w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
+    w[8] = 0x80000000u;
+#pragma unroll
+    for (int j = 9; j < 14; ++j) w[j] = 0;
+  } else {
+    w[0] = 0x80000000u;
+#pragma unroll
+    for (int j = 1; j < 14; ++j) w[j] = 0;
+  }
+  const uint64_t bits = 256 * cnt;
+  w[14] = (uint32_t)(bits >> 32);
+  w[15] = (uint32_t)bits;
+}
+
+struct DigestSrc {
+  const uint8_t* table;
+  const uint32_t* idx;
+  const uint64_t* begin;
+  struct Msg {
+    uint64_t k0, cnt;
+    uint8_t* slot;
+    uint32_t nb;
+    bool ok;
+  };
+  template <int MODE>
+  __device__ __forceinline__ void full(uint64_t i, uint8_t* out) const {
+    const uint64_t k0 = begin[i], cnt = begin[i + 1] - k0;
+    const uint4* tab = reinterpret_cast<const uint4*>(table);
+    State s;
+    state_init(s);
+    uint32_t w[16];
+    uint64_t k = 0;
+    for (; k + 2 <= cnt; k += 2) {
+      dod_pair_block(tab, idx + k0, k, w);
+      compress(s, w);
+    }
+    dod_final_block(tab, idx + k0, k, cnt, w);
+    compress(s, w);
+    store_digest(s, out + 32 * i);
+  }
+  __device__ __forceinline__ Msg open(uint64_t i, uint32_t, uint8_t* out) const {
+    Msg g;
+    g.k0 = begin[i];
+    g.cnt = begin[i + 1] - g.k0;
+    g.slot = out + 32 * i;
+    g.nb = (uint32_t)(g.cnt / 2 + 1);
+    g.ok = true;
+    return g;
+  }
+  __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1) const {
+    const uint4* tab = reinterpret_cast<const uint4*>(table);
+    uint32_t w[16];
+    for (uint32_t b = b0; b < b1; ++b) {
+      if (b < g.cnt / 2) dod_pair_block(tab, idx + g.k0, 2 * (uint64_t)b, w);
+      else dod_final_block(tab, idx + g.k0, 2 * (uint64_t)b, g.cnt, w);
+      compress(st, w);
+    }
+  }
+};
+
+template <int MODE, class Src>
+__global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, uint8_t* __restrict__ out,
+                                                      uint32_t* __restrict__ err, SplitPlan sp) {
+  const uint32_t seg_wgs = sp.segments * sp.groups;
+  if (blockIdx.x >= seg_wgs) {  // main workgroups: one lane per message, [0, n_main)
+    const uint64_t i = (uint64_t)(blockIdx.x - seg_wgs) * blockDim.x + threadIdx.x;
+    if (i < sp.n_main) src.template full<MODE>(i, out);
+    return;
+  }
+  const uint32_t seg = blockIdx.x / sp.groups;
+  const uint32_t chain = (blockIdx.x % sp.groups) * 4 + threadIdx.x / 64;
+  if (chain >= sp.chains) return;  // whole wave
+  __builtin_amdgcn_s_setprio(3);
+  const uint32_t lane = threadIdx.x & 63;
+  uint64_t* flag = sp.flags + chain;
+  if (seg > 0) {  // wait for segment seg-1 of this chain (same launch: same epoch)
+    const uint64_t want = (sp.epoch << 8) | seg;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+      __builtin_amdgcn_s_sleep(8);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kSplitWaitTicks) {
+        if (lane == 0) {
+          atomicOr(err, 2u);
+          __hip_atomic_store(flag, want + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        return;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  }
+  const uint64_t i = sp.n_main + (uint64_t)chain * 64 + lane;
+  if (i < n) {
+    const typename Src::Msg g = src.open(i, seg, out);
+    if (g.ok) {
+      const uint32_t b0 = (uint32_t)((uint64_t)g.nb * seg / sp.segments);
+      const uint32_t b1 = (uint32_t)((uint64_t)g.nb * (seg + 1) / sp.segments);
+      State st;
+      if (seg == 0) {
+        state_init(st);
+      } else {  // the previous segment's state, parked in this message's digest slot
+        const uint4 lo = reinterpret_cast<const uint4*>(g.slot)[0];
+        const uint4 hi = reinterpret_cast<const uint4*>(g.slot)[1];
+        st.h[0] = lo.x; st.h[1] = lo.y; st.h[2] = lo.z; st.h[3] = lo.w;
+        st.h[4] = hi.x; st.h[5] = hi.y; st.h[6] = hi.z; st.h[7] = hi.w;
+      }
+      src.blocks(g, st, b0, b1);
+      if (seg + 1 == sp.segments) {
+        store_digest(st, g.slot);
+      } else {  // raw state words, resumed by the next segment
+        reinterpret_cast<uint4*>(g.slot)[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+        reinterpret_cast<uint4*>(g.slot)[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+      }
+    }
+  }
+  if (seg + 1 < sp.segments) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    if (lane == 0)
+      __hip_atomic_store(flag, (sp.epoch << 8) | (seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -309,41 +533,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_of_digests(const uint8_t* __r
                                                            uint64_t n, uint8_t* __restrict__ out) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t k0 = begin[i], cnt = begin[i + 1] - k0;
-  const uint64_t len = 32 * cnt;
-  const uint4* tab = reinterpret_cast<const uint4*>(table);
-  State s;
-  state_init(s);
-  uint32_t w[16];
-  uint64_t k = 0;
-  for (; k + 2 <= cnt; k += 2) {
-    const uint4* d0 = tab + 2 * (uint64_t)idx[k0 + k];
-    const uint4* d1 = tab + 2 * (uint64_t)idx[k0 + k + 1];
-    uint4 v0 = d0[0], v1 = d0[1], v2 = d1[0], v3 = d1[1];
-    w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
-    w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
-    w[8] = bswap(v2.x); w[9] = bswap(v2.y); w[10] = bswap(v2.z); w[11] = bswap(v2.w);
-    w[12] = bswap(v3.x); w[13] = bswap(v3.y); w[14] = bswap(v3.z); w[15] = bswap(v3.w);
-    compress(s, w);
-  }
-  const uint64_t bits = len * 8;
-  if (k < cnt) {  // one digest left: 32 bytes + 0x80 + zeros + length fit one block
-    const uint4* d0 = tab + 2 * (uint64_t)idx[k0 + k];
-    uint4 v0 = d0[0], v1 = d0[1];
-    w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
-    w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
-    w[8] = 0x80000000u;
-#pragma unroll
-    for (int j = 9; j < 14; ++j) w[j] = 0;
-  } else {
-    w[0] = 0x80000000u;
-#pragma unroll
-    for (int j = 1; j < 14; ++j) w[j] = 0;
-  }
-  w[14] = (uint32_t)(bits >> 32);
-  w[15] = (uint32_t)bits;
-  compress(s, w);
-  store_digest(s, out + 32 * i);
+  DigestSrc{table, idx, begin}.full<0>(i, out);
 }
 
 // ---------------------------------------------------------------------------
@@ -385,10 +575,39 @@ static inline void with_mode(int mode, F&& f) {
   }
 }
 
+// Split chaining (AUTO and LANE) when the launch is q >= 2 full rounds of waves
+// over the SIMDs plus a surplus of r <= SIMDs/2 waves: r chains of
+// clamp(SIMDs / r, 2, 8) segments, so no SIMD carries more than one segment.
+bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp) {
+  static const int forced = env_int("MSHA_SPLIT", -1);  // A/B: 0 = never
+  if (forced == 0 || policy == 2) return false;
+  const uint64_t simds = (uint64_t)cus * 4;
+  const uint64_t waves = (n + 63) / 64;
+  const uint64_t q = waves / simds, r = waves % simds;
+  if (q < 2 || r == 0 || r > simds / 2) return false;
+  sp->n_main = q * simds * 64;
+  sp->chains = (uint32_t)r;
+  sp->segments = (uint32_t)std::min<uint64_t>(8, std::max<uint64_t>(2, simds / r));
+  // 4 chains per 256-thread workgroup; a multiple of 8 workgroups per segment
+  // keeps a chain's segments on one XCD (workgroup id mod 8)
+  sp->groups = (uint32_t)(((r + 3) / 4 + 7) / 8 * 8);
+  return true;
+}
+
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
                                const uint32_t* order, const uint32_t* out_idx, uint64_t n,
-                               uint8_t* out, uint32_t* err, int cus, int policy, hipStream_t st) {
+                               uint8_t* out, uint32_t* err, int cus, int policy, hipStream_t st,
+                               const SplitPlan* split) {
   if (n == 0) return hipSuccess;
+  if (split) {
+    const unsigned grid = split->segments * split->groups + (unsigned)(split->n_main / 256);
+    const ArenaSrc src{arena, off, len, order, out_idx, err};
+    with_mode(pick_mode(split->n_main, cus), [&](auto m) {
+      hipLaunchKernelGGL((k_digest_split<decltype(m)::value, ArenaSrc>), dim3(grid), dim3(256), 0,
+                         st, src, n, out, err, *split);
+    });
+    return hipGetLastError();
+  }
   if (uses_coop(n, cus, policy)) {
     const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
     hipLaunchKernelGGL(k_digest_coop<kPrefetch>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len,
@@ -415,8 +634,14 @@ hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t
 
 hipError_t launch_digest_of_digests(const uint8_t* table, const uint32_t* idx,
                                     const uint64_t* begin, uint64_t n, uint8_t* out,
-                                    hipStream_t st) {
+                                    uint32_t* err, hipStream_t st, const SplitPlan* split) {
   if (n == 0) return hipSuccess;
+  if (split) {
+    const unsigned grid = split->segments * split->groups + (unsigned)(split->n_main / 256);
+    hipLaunchKernelGGL((k_digest_split<0, DigestSrc>), dim3(grid), dim3(256), 0, st,
+                       DigestSrc{table, idx, begin}, n, out, err, *split);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(k_digest_of_digests, dim3(grid_for(n)), dim3(256), 0, st, table, idx, begin,
                      n, out);
   return hipGetLastError();

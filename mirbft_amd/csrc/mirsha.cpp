@@ -109,8 +109,14 @@ struct Device {
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
   uint64_t direct_lo = 0;         // direct mode: first caller-arena byte uploaded
+  // split chaining (kernels.hip): kSplitRing flag arrays of cus*2 entries,
+  // allocated once and zeroed, never reallocated (launches may be in flight)
+  uint64_t* split_flags = nullptr;
+  uint64_t split_epoch = 0;
   void release() {
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table}) b->release();
+    if (split_flags) (void)hipFree(split_flags);
+    split_flags = nullptr;
     for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1]}) b->release();
     for (hipEvent_t* e : {&ev0, &ev1, &slot_free[0], &slot_free[1], &chunk_in}) {
       if (*e) (void)hipEventDestroy(*e);
@@ -123,6 +129,22 @@ struct Device {
     stream = copy_stream = nullptr;
   }
 };
+
+// Split-chaining plan for an n-message launch on d (nullptr: plain launch).
+// Consecutive launches use different flag arrays of a ring and unique epochs,
+// so a launch never reads another launch's flags.
+constexpr uint64_t kSplitRing = 16;
+const msha::SplitPlan* split_for(Device& d, uint64_t n, int policy, msha::SplitPlan& sp) {
+  if (!msha::plan_split(n, d.cus, policy, &sp)) return nullptr;
+  const uint64_t per = (uint64_t)d.cus * 2;  // plan_split: chains <= SIMDs / 2
+  if (!d.split_flags) {
+    HIPCHK(hipMalloc(&d.split_flags, kSplitRing * per * sizeof(uint64_t)));
+    HIPCHK(hipMemset(d.split_flags, 0, kSplitRing * per * sizeof(uint64_t)));
+  }
+  sp.epoch = ++d.split_epoch;
+  sp.flags = d.split_flags + (sp.epoch % kSplitRing) * per;
+  return &sp;
+}
 
 // MSHA_TRACE=1: host-side phase timestamps (ms since the call began) on stderr.
 inline void trace(const char* what, double t0) {
@@ -858,11 +880,12 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       P.launched = q1;
       // off/len are lane-indexed; out_idx maps lane -> shard-local message
       // (identity placement: lane q is message q)
+      msha::SplitPlan sp;
       HIPCHK(msha::launch_digest_batch(
           d.arena.as<uint8_t>(), d.off.as<uint64_t>() + l0, d.len.as<uint64_t>() + l0, nullptr,
           P.ordered ? d.order.as<uint32_t>() + l0 : nullptr, lanes,
           d.out.as<uint8_t>() + (P.ordered ? 0 : 32 * l0), d.err.as<uint32_t>(), d.cus,
-          ctx->kernel_policy, d.stream));
+          ctx->kernel_policy, d.stream, split_for(d, lanes, ctx->kernel_policy, sp)));
       // Identity lanes: these digests are final, bring them back while later
       // chunks upload and hash (into the caller's buffer itself if it is pinned).
       if (P.identity())
@@ -893,6 +916,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     kernel_ms = std::max<double>(kernel_ms, ms);
     uint32_t errflag;
     std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+    if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out");
     if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
     const std::vector<uint32_t>& rep = plans[s].rep;
     const uint8_t* h = d.h_out.as<uint8_t>();
@@ -1164,12 +1188,18 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
       if (n_table) HIPCHK(hipMemcpyAsync(d.table.p, table, 32 * n_table, hipMemcpyHostToDevice, d.stream));
       if (i1 > i0) HIPCHK(hipMemcpyAsync(d.idx.p, idx + i0, 4 * (i1 - i0), hipMemcpyHostToDevice, d.stream));
       HIPCHK(hipMemcpyAsync(d.begin.p, hb, 8 * (m + 1), hipMemcpyHostToDevice, d.stream));
+      d.err.ensure(4);
+      HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
       HIPCHK(hipEventRecord(d.ev0, d.stream));
+      msha::SplitPlan sp;
       HIPCHK(msha::launch_digest_of_digests(d.table.as<uint8_t>(), d.idx.as<uint32_t>(),
-                                            d.begin.as<uint64_t>(), m, d.out.as<uint8_t>(), d.stream));
+                                            d.begin.as<uint64_t>(), m, d.out.as<uint8_t>(),
+                                            d.err.as<uint32_t>(), d.stream,
+                                            split_for(d, m, ctx->kernel_policy, sp)));
       HIPCHK(hipEventRecord(d.ev1, d.stream));
-      d.h_out.ensure(32 * m);
+      d.h_out.ensure(32 * m + 4);
       HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+      HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
     }
     double kernel_ms = 0;
     for (uint32_t s = 0; s < k; ++s) {
@@ -1181,6 +1211,9 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
       kernel_ms = std::max<double>(kernel_ms, ms);
+      uint32_t errflag;
+      std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+      if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out");
       std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
     }
     uint64_t blocks = 0;
@@ -1200,7 +1233,10 @@ static int device_prologue(msha_ctx* ctx, void* stream, hipStream_t* st) {
   if (!ctx || ctx->devs.empty()) return MSHA_ERR_INVALID_ARG;
   Device& d = ctx->devs[0];
   HIPCHK(hipSetDevice(d.id));
-  d.err.ensure(4);
+  if (!d.err.p) {  // first device call: a zeroed error word (hipMalloc does not zero)
+    d.err.ensure(4);
+    HIPCHK(hipMemset(d.err.p, 0, 4));
+  }
   *st = stream ? static_cast<hipStream_t>(stream) : d.stream;
   return MSHA_OK;
 }
@@ -1215,8 +1251,10 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
     hipStream_t st;
     device_prologue(ctx, stream, &st);
     Device& d = ctx->devs[0];
+    msha::SplitPlan sp;
     HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, d_order, nullptr, n, d_out,
-                                     d.err.as<uint32_t>(), d.cus, ctx->kernel_policy, st));
+                                     d.err.as<uint32_t>(), d.cus, ctx->kernel_policy, st,
+                                     split_for(d, n, ctx->kernel_policy, sp)));
   });
 }
 
@@ -1242,7 +1280,10 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
   return guarded(ctx, [&] {
     hipStream_t st;
     device_prologue(ctx, stream, &st);
-    HIPCHK(msha::launch_digest_of_digests(d_table, d_idx, d_begin, n, d_out, st));
+    Device& d = ctx->devs[0];
+    msha::SplitPlan sp;
+    HIPCHK(msha::launch_digest_of_digests(d_table, d_idx, d_begin, n, d_out, d.err.as<uint32_t>(), st,
+                                          split_for(d, n, ctx->kernel_policy, sp)));
   });
 }
 
@@ -1266,6 +1307,7 @@ int msha_device_status(msha_ctx* ctx) {
     HIPCHK(hipMemset(d.err.p, 0, 4));
   });
   if (rc != MSHA_OK) return rc;
+  if (flag & 2) return fail(ctx, MSHA_ERR_HIP, "split-chain handoff timed out (digests undefined)");
   if (flag) return fail(ctx, MSHA_ERR_ALIGNMENT, "device arena message start not 16-byte aligned");
   return MSHA_OK;
 }

@@ -446,3 +446,65 @@ def test_pinned_direct_chunked_sharded(monkeypatch):
         assert np.array_equal(e.digest_batch(p2, w2.off, w2.len),
                               oracle.digest_batch(w2.arena, w2.off, w2.len))
         assert e.stats()["direct_calls"] == 2
+
+
+def _cus():
+    import torch
+    return torch.cuda.get_device_properties(0).multi_processor_count
+
+
+@pytest.mark.parametrize("surplus_waves,tail", [(1, 0), (6, 17), (53, 0), (None, 5)])
+def test_split_chaining_tail(engine, surplus_waves, tail):
+    """Launches of q >= 2 full rounds of waves plus a surplus of 1..SIMDs/2 waves
+    run the surplus as split chains (a message's state handed between segment
+    waves); every digest bit-exact vs the oracle, with and without a lane order,
+    mixed lengths (segments of 0 blocks included), and through the host API."""
+    import torch
+    simds = _cus() * 4
+    r = surplus_waves if surplus_waves is not None else simds // 2    # max surplus
+    n = 2 * simds * 64 + r * 64 - (64 - tail if tail else 0)
+    rng = np.random.default_rng(r)
+    lens = rng.choice(np.array([0, 55, 56, 64, 119, 640, 1000], dtype=np.uint64), size=n)
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum((lens + np.uint64(15)) & ~np.uint64(15))[:-1]
+    arena = W.random_bytes(7, 0, int(offs[-1] + lens[-1]) + 128)
+    w = W.Workload("split", arena, offs, lens)
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    d_arena, d_off, d_len = _to_dev(w)
+    out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device(d_arena, d_off, d_len, out)
+    engine.device_status()
+    assert np.array_equal(out.cpu().numpy(), exp)
+    from mirbft_amd.engine import order_by_blocks
+    d_order = torch.from_numpy(order_by_blocks(w.len).view(np.int32)).to("cuda:0")
+    out.zero_()
+    engine.digest_batch_device(d_arena, d_off, d_len, out, order=d_order)
+    engine.device_status()
+    assert np.array_equal(out.cpu().numpy(), exp)
+    # host API (lane-indexed metadata + out_idx through the pipeline)
+    assert np.array_equal(engine.digest_batch(w.arena, w.off, w.len), exp)
+
+
+@pytest.mark.parametrize("surplus_waves,tail", [(1, 0), (7, 33), (None, 0)])
+def test_split_chaining_digest_of_digests(engine, surplus_waves, tail):
+    """Digest-of-digests launches with a surplus of waves run the surplus as split
+    chains; ragged digest counts (0, 1, odd, even, up to 40) so segments start on
+    pair blocks, the odd-digest final block and the length-only final block."""
+    import torch
+    simds = _cus() * 4
+    r = surplus_waves if surplus_waves is not None else simds // 2
+    n = 2 * simds * 64 + r * 64 - (64 - tail if tail else 0)
+    rng = np.random.default_rng(100 + r)
+    table = rng.integers(0, 256, size=(4096, 32), dtype=np.uint8)
+    cnt = rng.choice(np.array([0, 1, 2, 3, 19, 20, 40], dtype=np.uint64), size=n)
+    begin = np.zeros(n + 1, dtype=np.uint64)
+    begin[1:] = np.cumsum(cnt)
+    idx = rng.integers(0, table.shape[0], size=int(begin[-1]), dtype=np.uint32)
+    exp = oracle.digest_of_digests(table, idx, begin)
+    out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_of_digests_device(torch.from_numpy(table).to("cuda:0"),
+                                    torch.from_numpy(idx.view(np.int32)).to("cuda:0"),
+                                    torch.from_numpy(begin.view(np.int64)).to("cuda:0"), out)
+    engine.device_status()
+    assert np.array_equal(out.cpu().numpy(), exp)
+    assert np.array_equal(engine.digest_of_digests(table, idx, begin), exp)
