@@ -159,27 +159,48 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
 // and a flag; segment s+1 (another workgroup, so usually another SIMD) waits for
 // that flag. Each SIMD then carries at most ~1/S_seg of a surplus wave instead
 // of a whole one. Segment workgroups come first in the grid and a segment
-// only ever waits on a lower workgroup id (dispatched before it), so every
-// wait is on a resident or finished wave; a wait longer than 100 ms (never
-// expected) raises error bit 2 and unblocks the chain, so every wave exits.
+// only ever waits on a lower workgroup id of its own XCD (dispatched before
+// it), so every wait is on a resident or finished wave.
+//
+// A chain's flag word: epoch (bits 63..40) | segments done (39..32) | beat.
+// The running segment stores a new beat every block, so a waiter can tell a
+// long chain (huge messages) from a stuck one: only 100 ms without any
+// change of the word (never expected) raises error bit 2 and unblocks the
+// chain, so every wave exits.
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSplitWaitTicks = 10000000;  // 100 ms of s_memrealtime (100 MHz)
+
+__device__ __forceinline__ uint64_t split_word(uint64_t epoch, uint32_t done, uint32_t beat) {
+  return ((epoch & 0xFFFFFFu) << 40) | ((uint64_t)(done & 0xFFu) << 32) | beat;
+}
+
+// Progress beat of the running segment, every 8 blocks (one store per ~20 us;
+// a beat per block cost c3 1.5 %). ArenaSrc beats between 8-block runs of its
+// block loop: a conditional store inside that loop made the compiler spill.
+constexpr uint32_t kBeatBlocks = 8;
+struct Beat {
+  uint64_t* flag;
+  uint64_t base;
+  __device__ __forceinline__ void operator()(uint32_t b) const {
+    __hip_atomic_store(flag, base | b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+};
 
 // Blocks [b0, b1) of the message at p (len bytes), state in/out in s.
 __device__ __forceinline__ void hash_blocks(State& s, const uint8_t* p, uint64_t len, uint32_t b0,
                                             uint32_t b1) {
   const uint32_t nfull = (uint32_t)(len >> 6);
   const uint32_t r = (uint32_t)(len & 63);
-  uint32_t raw[16];
-  uint32_t w[16];
+  uint32_t w[16];  // loaded, then byte-swapped / masked in place (no second array)
   for (uint32_t b = b0; b < b1; ++b) {
-    if (b <= nfull) load_block16(p + 64 * (uint64_t)b, raw);
+    if (b <= nfull) load_block16(p + 64 * (uint64_t)b, w);
     if (b < nfull) {
-      to_words(raw, w);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
     } else if (b == nfull) {
       uint32_t rr = r;
       asm volatile("" : "+v"(rr));
-      build_tail(raw, rr, len, w);
+      build_tail(w, rr, len, w);
     } else {
       length_block(len, w);
     }
@@ -223,8 +244,12 @@ struct ArenaSrc {  // messages arena[off[m] : off[m]+len[m]] (k_digest_batch's f
     g.ok = seg == 0 ? check_aligned(g.p, g.slot, err) : (reinterpret_cast<uintptr_t>(g.p) & 15) == 0;
     return g;
   }
-  __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1) const {
-    hash_blocks(st, g.p, g.len, b0, b1);
+  __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1,
+                                         const Beat& beat) const {
+    for (uint32_t c = b0; c < b1; c += kBeatBlocks) {
+      hash_blocks(st, g.p, g.len, c, std::min(c + kBeatBlocks, b1));
+      beat(c);
+    }
   }
 };
 
@@ -296,13 +321,15 @@ struct DigestSrc {
     g.ok = true;
     return g;
   }
-  __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1) const {
+  __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1,
+                                         const Beat& beat) const {
     const uint4* tab = reinterpret_cast<const uint4*>(table);
     uint32_t w[16];
     for (uint32_t b = b0; b < b1; ++b) {
       if (b < g.cnt / 2) dod_pair_block(tab, idx + g.k0, 2 * (uint64_t)b, w);
       else dod_final_block(tab, idx + g.k0, 2 * (uint64_t)b, g.cnt, w);
       compress(st, w);
+      if (b % kBeatBlocks == 0) beat(b);  // spill-free here (53 VGPRs)
     }
   }
 };
@@ -322,21 +349,29 @@ __global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, ui
   __builtin_amdgcn_s_setprio(3);
   const uint32_t lane = threadIdx.x & 63;
   uint64_t* flag = sp.flags + chain;
-  if (seg > 0) {  // wait for segment seg-1 of this chain (same launch: same epoch)
-    const uint64_t want = (sp.epoch << 8) | seg;
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != want) {
+  const uint64_t ep = split_word(sp.epoch, 0, 0);
+  if (seg > 0) {  // wait until seg segments of this chain are done (same launch: same epoch)
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while ((seen >> 40) != (ep >> 40) || ((seen >> 32) & 0xFF) < seg) {
       __builtin_amdgcn_s_sleep(8);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kSplitWaitTicks) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      const uint64_t v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (v != seen) {  // the chain moved (a beat or a handoff): restart the clock
+        seen = v;
+        t0 = now;
+      } else if (now - t0 > kSplitWaitTicks) {
         if (lane == 0) {
           atomicOr(err, 2u);
-          __hip_atomic_store(flag, want + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(flag, split_word(sp.epoch, seg + 1, 0), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
         }
         return;
       }
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
+  const Beat beat{flag, split_word(sp.epoch, seg, 0)};
   const uint64_t i = sp.n_main + (uint64_t)chain * 64 + lane;
   if (i < n) {
     const typename Src::Msg g = src.open(i, seg, out);
@@ -352,7 +387,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, ui
         st.h[0] = lo.x; st.h[1] = lo.y; st.h[2] = lo.z; st.h[3] = lo.w;
         st.h[4] = hi.x; st.h[5] = hi.y; st.h[6] = hi.z; st.h[7] = hi.w;
       }
-      src.blocks(g, st, b0, b1);
+      src.blocks(g, st, b0, b1, beat);
       if (seg + 1 == sp.segments) {
         store_digest(st, g.slot);
       } else {  // raw state words, resumed by the next segment
@@ -364,7 +399,8 @@ __global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, ui
   if (seg + 1 < sp.segments) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (lane == 0)
-      __hip_atomic_store(flag, (sp.epoch << 8) | (seg + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(flag, split_word(sp.epoch, seg + 1, 0), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 

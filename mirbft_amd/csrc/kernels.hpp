@@ -21,9 +21,9 @@ struct SplitPlan {
   uint32_t chains = 0;      // surplus waves: messages [n_main, n) in chains of 64
   uint32_t segments = 0;    // segments per chain
   uint32_t groups = 0;      // segment workgroups per segment (4 chains each, padded)
-  uint64_t epoch = 0;       // unique per launch on this flags array (< 2^56)
-  uint64_t* flags = nullptr;  // device, >= chains entries; segment s of this launch
-                              // is published as (epoch << 8) | (s + 1)
+  uint64_t epoch = 0;       // unique (mod 2^24) among the launches that share flags
+  uint64_t* flags = nullptr;  // device, >= chains entries, one word per chain:
+                              // epoch | segments done | progress beat (kernels.hip)
 };
 bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp);
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,

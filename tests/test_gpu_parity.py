@@ -508,3 +508,24 @@ def test_split_chaining_digest_of_digests(engine, surplus_waves, tail):
     engine.device_status()
     assert np.array_equal(out.cpu().numpy(), exp)
     assert np.array_equal(engine.digest_of_digests(table, idx, begin), exp)
+
+
+def test_split_chaining_long_surplus_message(engine):
+    """A 32 MiB message among the surplus waves of an unordered launch: its chain's
+    segments run ~0.2 s each, far past the handoff timeout, but the running segment's
+    per-block progress beat keeps the waiting segments from timing out."""
+    import torch
+    simds = _cus() * 4
+    n = 2 * simds * 64 + 64
+    lens = np.full(n, 64, dtype=np.uint64)
+    lens[-3] = 32 << 20
+    offs = np.zeros(n, dtype=np.uint64)
+    offs[1:] = np.cumsum((lens + np.uint64(15)) & ~np.uint64(15))[:-1]
+    arena = W.random_bytes(11, 0, int(offs[-1] + lens[-1]) + 128)
+    w = W.Workload("split-long", arena, offs, lens)
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    d_arena, d_off, d_len = _to_dev(w)
+    out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device(d_arena, d_off, d_len, out)
+    engine.device_status()
+    assert np.array_equal(out.cpu().numpy(), exp)

@@ -2,7 +2,7 @@
 set -u
 mkdir -p gpurun_out/split
 export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "split or c3 or c5 or alias or chunked" > gpurun_out/split/pytest.log 2>&1; rc=$?
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread -k "split or c3 or c5 or alias or chunked or digest_of" > gpurun_out/split/pytest.log 2>&1; rc=$?
 tail -3 gpurun_out/split/pytest.log; [ $rc -ne 0 ] && exit $rc
 for rep in 1 2; do
   for sp in 0 1; do
