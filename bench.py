@@ -19,7 +19,9 @@ reports warmup_steps_run and warmup_ms.
 
 roofline: the kernel is integer-VALU bound. achieved = 1400 int32 ops per
 64-byte block (the minimal gfx950 instruction count) x blocks per
-launch / mean launch time (HIP events on the launch stream); peak = 78.64 T
+launch / mean launch time (one HIP event pair on the launch stream around the
+K timed launches, divided by K: dispatch gaps included; an event pair around
+every launch -- --events step -- itself cost c3 8 % per step); peak = 78.64 T
 lane-ops/s (256 CU x 4 SIMD-32 x 2.4 GHz, MI355X_MICROARCH.md). cpu_baseline:
 the oracle's single-threaded C restatement of the same loop on a bounded
 sample, rank 0 only.
@@ -69,6 +71,9 @@ def parse():
     p.add_argument("--pinned", action="store_true",
                    help="with --e2e: the batch is packed in pinned host memory (msha_pinned_alloc), "
                         "as a cgo adapter would, so the library DMAs it as is")
+    p.add_argument("--events", default="span", choices=["step", "span"],
+                   help="span: one HIP event pair around the K launches (default); step: a pair "
+                        "around every launch (costs c3 8%% per step: the A/B of the events' cost)")
     p.add_argument("--share-device", action="store_true",
                    help="rehearsal only: every rank uses GPU 0 (multi-rank path on a 1-GPU box)")
     return p.parse_args()
@@ -274,15 +279,21 @@ def main():
     eng.device_status()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
+           for _ in range(args.steps if args.events == "step" else 1)]
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(stream)
-        step()
-        e1.record(stream)
+    if args.events == "step":
+        for e0, e1 in evs:
+            e0.record(stream)
+            step()
+            e1.record(stream)
+    else:
+        evs[0][0].record(stream)
+        for _ in range(args.steps):
+            step()
+        evs[0][1].record(stream)
     torch.cuda.synchronize(dev)
     # This rank's span ends when its GPU has drained; the closing barrier (and
     # the max over ranks below) then gives the job's makespan without charging
@@ -291,6 +302,8 @@ def main():
     if world > 1:
         dist.barrier()
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if args.events == "span":
+        kern_ms /= args.steps
     eng.device_status()
     if not (args.config.startswith("u:") and w.uniform_stride != (int(w.len[0]) + 15) // 16 * 16):
         verify_sample(w, d_out)
