@@ -308,8 +308,19 @@ struct DigestSrc {
       dod_pair_block(tab, idx + k0, k, w);
       compress(s, w);
     }
-    dod_final_block(tab, idx + k0, k, cnt, w);
-    compress(s, w);
+    // A wave-uniform even count (the Batch shape: BatchSize acks per batch) leaves a
+    // final block of padding and length only, the same for every lane: its schedule
+    // runs on the SALU (compress_uniform_pad), the VALU does only the rounds.
+    const uint32_t c_lo = __builtin_amdgcn_readfirstlane((uint32_t)cnt);
+    const uint32_t c_hi = __builtin_amdgcn_readfirstlane((uint32_t)(cnt >> 32));
+    const uint64_t cnt0 = ((uint64_t)c_hi << 32) | c_lo;
+    if (__ballot(cnt != cnt0) == 0 && !(c_lo & 1)) {
+      const uint64_t bits = 256 * cnt0;
+      compress_uniform_pad(s, 0x80000000u, (uint32_t)(bits >> 32), (uint32_t)bits);
+    } else {
+      dod_final_block(tab, idx + k0, k, cnt, w);
+      compress(s, w);
+    }
     store_digest(s, out + 32 * i);
   }
   __device__ __forceinline__ Msg open(uint64_t i, uint32_t, uint8_t* out) const {

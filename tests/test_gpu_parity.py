@@ -510,6 +510,32 @@ def test_split_chaining_digest_of_digests(engine, surplus_waves, tail):
     assert np.array_equal(engine.digest_of_digests(table, idx, begin), exp)
 
 
+@pytest.mark.parametrize("count", [0, 1, 2, 3, 20, 21, 40, 1000])
+@pytest.mark.parametrize("split", [False, True])
+def test_digest_of_digests_uniform_counts(engine, count, split):
+    """Whole waves of Batch digests with one digest count: an even count takes the
+    wave-uniform final block (length-only, schedule on the SALU), an odd one the VALU
+    final block; 0 parts is SHA256(""). split: a launch with surplus waves (split chains)."""
+    import torch
+    if split and count > 40:
+        pytest.skip("oracle time: the split launch is >= 131 K Batches")
+    n = 2 * _cus() * 4 * 64 + 3 * 64 + 5 if split else 64 * 6 + 5
+    rng = np.random.default_rng(200 + count)
+    table = rng.integers(0, 256, size=(2048, 32), dtype=np.uint8)
+    begin = np.arange(n + 1, dtype=np.uint64) * np.uint64(count)
+    idx = rng.integers(0, table.shape[0], size=int(begin[-1]), dtype=np.uint32)
+    exp = oracle.digest_of_digests(table, idx, begin)
+    if count == 0:
+        idx = np.zeros(1, dtype=np.uint32)   # no part is read, but the device API takes no null pointer
+        assert bytes(exp[0]) == hashlib.sha256(b"").digest()
+    out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_of_digests_device(torch.from_numpy(table).to("cuda:0"),
+                                    torch.from_numpy(idx.view(np.int32)).to("cuda:0"),
+                                    torch.from_numpy(begin.view(np.int64)).to("cuda:0"), out)
+    engine.device_status()
+    assert np.array_equal(out.cpu().numpy(), exp)
+
+
 def test_split_chaining_long_surplus_message(engine):
     """A 32 MiB message among the surplus waves of an unordered launch: its chain's
     segments run ~0.2 s each, far past the handoff timeout, but the running segment's
