@@ -53,7 +53,7 @@ __device__ __forceinline__ void to_words(const uint32_t (&raw)[16], uint32_t (&w
 //            the two half-line requests (lane stride >= 128 B is the norm)
 // (Rejected after A/B, profiles/r01_ab_modes, r01_ab_nt: an LDS-DMA prefetch
 // mode, 6 % slower on c2, and nontemporal payload loads, 5-10 % slower.)
-enum LoadMode { kSingle = 0, kPrefetch = 1, kPair = 2 };
+enum LoadMode { kSingle = 0, kPrefetch = 1, kPair = 2, kPipe = 3 };
 
 // Hash one message of `len` bytes starting at p (device memory, 16-byte
 // aligned, with kArenaSlack (kernels.hpp) readable bytes after the arena's last
@@ -118,6 +118,119 @@ __device__ __forceinline__ void hash_message(const uint8_t* p, uint64_t len, uin
   store_digest(s, out);
 }
 
+// ---------------------------------------------------------------------------
+// Software-pipelined lane kernel (kPipe) for launches of about one wave per
+// SIMD (few, long messages: c4's 65,536 x 64 KiB is exactly 1,024 waves on
+// 1,024 SIMDs). A lone wave issues a VALU instruction only every ~4.6 cycles
+// (vs ~3.9 with 2+ waves): nothing else on the SIMD fills the gaps
+// of the round chain, and in compress() rounds 0-15 have no schedule work at
+// all. Here block b's 64 rounds consume a fully expanded schedule W[64], and
+// the same straight-line code expands block b+1's schedule (independent of
+// the rounds) into a second array, one word per round; the raw bytes of block
+// b+2 are loaded at the top of the step. Two schedule arrays and two raw
+// buffers ping-pong, so nothing is copied. ~190 VGPRs: one wave per SIMD.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void expand_block(const uint32_t (&raw)[16], uint32_t (&N)[64]) {
+#pragma unroll
+  for (int i = 0; i < 64; ++i)
+    N[i] = i < 16 ? bswap(raw[i]) : sig1(N[i - 2]) + N[i - 7] + sig0(N[i - 15]) + N[i - 16];
+}
+
+constexpr int pipe_slot(int j) { return j < 16 ? j / 4 : 4 + (j - 16) * 5 / 4; }
+
+// 64 rounds over the expanded W, interleaved word by word with the expansion
+// of `raw` (the next block) into N.
+__device__ __forceinline__ void rounds_expand(State& s, const uint32_t (&W)[64], uint32_t (&N)[64],
+                                              const uint32_t (&raw)[16]) {
+  constexpr uint32_t K[64] = {MSHA_K_TABLE};
+  uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
+  uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const uint32_t t1 = h + K[i] + W[i] + Sig1(e) + ch(e, f, g);
+    const uint32_t t2 = Sig0(a) + maj(a, b, c);
+    h = g; g = f; f = e; e = d + t1;
+    d = c; c = b; b = a; a = t1 + t2;
+    // Words due at round i (pipe_slot): byte swaps in rounds 0-3, then the 48
+    // expanded words spread evenly over rounds 4-62.
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int j = (i < 4 ? 4 * i : 16 + (i - 4) * 4 / 5) + k;
+      if (j < 64 && pipe_slot(j) == i) {
+        N[j] = j < 16 ? bswap(raw[j]) : sig1(N[j - 2]) + N[j - 7] + sig0(N[j - 15]) + N[j - 16];
+        asm volatile("" : "+v"(N[j]));
+      }
+    }
+    // Keep round i and its words together: left alone, instruction selection
+    // lumps the expansion into a few rounds and leaves the rest bare. Passing
+    // the values through an empty volatile asm orders them (emits nothing).
+    asm volatile("" : "+v"(a), "+v"(e));
+  }
+  s.h[0] += a; s.h[1] += b; s.h[2] += c; s.h[3] += d;
+  s.h[4] += e; s.h[5] += f; s.h[6] += g; s.h[7] += h;
+}
+
+__device__ __forceinline__ void hash_message_pipe(const uint8_t* p, uint64_t len, uint8_t* out) {
+  State s;
+  state_init(s);
+  const uint32_t nfull = (uint32_t)(len >> 6);
+  const uint32_t r = (uint32_t)(len & 63);
+  const uint32_t nblocks = nfull + (r < 56 ? 1 : 2);
+  const uint32_t len_lo0 = __builtin_amdgcn_readfirstlane((uint32_t)len);
+  const uint32_t len_hi0 = __builtin_amdgcn_readfirstlane((uint32_t)(len >> 32));
+  const uint64_t len0 = ((uint64_t)len_hi0 << 32) | len_lo0;
+  const bool uniform = __ballot(len != len0) == 0;
+  const uint32_t r0 = len_lo0 & 63;
+  const bool upad = uniform && (r0 == 0 || r0 >= 56);
+  const uint32_t nvalu = nblocks - (upad ? 1 : 0);
+  // Block j's bytes, clamped to the tail block (always readable: arena slack).
+  auto blk = [&](uint32_t j) { return p + 64 * (uint64_t)(j < nfull ? j : nfull); };
+  uint32_t tail[16];
+  if (nfull == 0) {
+    load_block16(p, tail);
+  } else {
+    uint32_t A[64], B[64], rawX[16], rawY[16];
+    load_block16(p, rawX);
+    expand_block(rawX, A);
+    load_block16(blk(1), rawX);
+    uint32_t b = 0;
+    for (;;) {
+      // A = schedule of block b, rawX = bytes of block b+1 (clamped)
+      load_block16(blk(b + 2), rawY);
+      rounds_expand(s, A, B, rawX);
+      if (++b >= nfull) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) tail[j] = rawX[j];
+        break;
+      }
+      // B = schedule of block b, rawY = bytes of block b+1 (clamped)
+      load_block16(blk(b + 2), rawX);
+      rounds_expand(s, B, A, rawY);
+      if (++b >= nfull) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) tail[j] = rawY[j];
+        break;
+      }
+    }
+  }
+  uint32_t w[16];
+  for (uint32_t b = nfull; b < nvalu; ++b) {
+    if (b == nfull) {
+      uint32_t rr = r;
+      asm volatile("" : "+v"(rr));
+      build_tail(tail, rr, len, w);
+    } else {
+      length_block(len, w);
+    }
+    compress(s, w);
+  }
+  if (upad) {
+    const uint64_t bits = len0 * 8;
+    compress_uniform_pad(s, r0 == 0 ? 0x80000000u : 0u, (uint32_t)(bits >> 32), (uint32_t)bits);
+  }
+  store_digest(s, out);
+}
+
 // Misaligned message start: not produced by the library's packers; flagged
 // (device word *err |= 1) and the digest zeroed rather than computed wrongly.
 __device__ __forceinline__ bool check_aligned(const uint8_t* p, uint8_t* out, uint32_t* err) {
@@ -143,6 +256,24 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
   const uint8_t* p = arena + off[m];
   if (check_aligned(p, out + 32 * o, err))
     hash_message<MODE>(p, len[m], out + 32 * o);
+}
+
+// k_digest_batch with the pipelined message loop; no occupancy hint (one wave
+// per SIMD is the design point, the VGPRs are the schedule arrays).
+__global__ __launch_bounds__(256) void k_digest_batch_pipe(const uint8_t* __restrict__ arena,
+                                                           const uint64_t* __restrict__ off,
+                                                           const uint64_t* __restrict__ len,
+                                                           const uint32_t* __restrict__ order,
+                                                           const uint32_t* __restrict__ out_idx,
+                                                           uint64_t n, uint8_t* __restrict__ out,
+                                                           uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t m = order ? (uint64_t)order[i] : i;
+  const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;
+  const uint8_t* p = arena + off[m];
+  if (check_aligned(p, out + 32 * o, err))
+    hash_message_pipe(p, len[m], out + 32 * o);
 }
 
 // ---------------------------------------------------------------------------
@@ -589,15 +720,19 @@ __global__ __launch_bounds__(256, 8) void k_digest_of_digests(const uint8_t* __r
 static inline unsigned grid_for(uint64_t n) { return (unsigned)((n + 255) / 256); }
 
 // Fewer than ~3 waves per SIMD cannot hide HBM latency by occupancy: use the
-// register-prefetching variant then; otherwise pair loads. For A/B
-// measurements MSHA_LOAD_MODE (0/1/2) forces the load mode.
+// register-prefetching variant then; otherwise pair loads. At one wave per
+// SIMD or less the pipelined kernel (kPipe, k_digest_batch_pipe) gives the lone
+// wave independent work: c4 2.78 -> 2.64 ms; at 1.5, 2 and 3 waves per SIMD it
+// ties or loses (profiles/r01_ab_pipe/). For A/B measurements MSHA_LOAD_MODE
+// (0/1/2/3) forces the load mode.
 static inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
 static inline int pick_mode(uint64_t n, int cus) {
   static const int forced = env_int("MSHA_LOAD_MODE", -1);
-  if (forced >= kSingle && forced <= kPair) return forced;
+  if (forced >= kSingle && forced <= kPipe) return forced;
+  if (n <= (uint64_t)cus * 4 * 64) return kPipe;
   return n < (uint64_t)cus * 4 * 64 * 3 ? kPrefetch : kPair;
 }
 
@@ -617,7 +752,9 @@ template <class F>
 static inline void with_mode(int mode, F&& f) {
   switch (mode) {
     case kSingle: f(std::integral_constant<int, kSingle>()); break;
-    case kPrefetch: f(std::integral_constant<int, kPrefetch>()); break;
+    case kPrefetch:
+    case kPipe:  // the pipelined loop has its own kernel (k_digest_batch_pipe)
+      f(std::integral_constant<int, kPrefetch>()); break;
     default: f(std::integral_constant<int, kPair>()); break;
   }
 }
@@ -665,7 +802,13 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
                        order, out_idx, n, out, err);
     return hipGetLastError();
   }
-  with_mode(pick_mode(n, cus), [&](auto m) {
+  const int mode = pick_mode(n, cus);
+  if (mode == kPipe) {
+    hipLaunchKernelGGL(k_digest_batch_pipe, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
+                       order, out_idx, n, out, err);
+    return hipGetLastError();
+  }
+  with_mode(mode, [&](auto m) {
     hipLaunchKernelGGL(k_digest_batch<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
                        arena, off, len, order, out_idx, n, out, err);
   });

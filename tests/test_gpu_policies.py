@@ -113,6 +113,36 @@ def test_large_messages(eng):
     assert eng.hash_actions([[m] for m in msgs]) == [hashlib.sha256(m).digest() for m in msgs]
 
 
+def _device_digests(engine, lens, salt):
+    import torch
+    lens = np.asarray(lens, dtype=np.uint64)
+    stride = (lens + 15) // 16 * 16
+    off = np.concatenate([[0], np.cumsum(stride)[:-1]]).astype(np.uint64)
+    arena = W.random_bytes(W.SEED ^ salt, 0, int(stride.sum()) + 64)
+    out = torch.empty((len(lens), 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device(_dev(arena), _dev(off), _dev(lens), out)
+    engine.device_status()
+    return out.cpu().numpy(), oracle.digest_batch(arena, off, lens)
+
+
+# The pipelined lane kernel (auto policy, n in (CUs*128, CUs*256]: one wave per
+# SIMD) exits its ping-pong loop after an odd or an even number of full blocks,
+# and hands wave-uniform padding-only final blocks to the SALU schedule.
+@pytest.mark.parametrize("size", [0, 55, 56, 63, 64, 119, 128, 183, 192, 200, 256, 1000])
+def test_pipe_uniform_lengths(engine, size):
+    got, want = _device_digests(engine, [size] * 40_000, 0x90 + size)
+    assert np.array_equal(got, want)
+
+
+def test_pipe_ragged_lengths(engine):
+    rng = np.random.default_rng(31)
+    lens = rng.integers(0, 1500, 50_000)
+    lens[::7] = rng.integers(0, 5, len(lens[::7])) * 64   # exact block multiples
+    lens[3::7] = rng.integers(0, 5, len(lens[3::7])) * 64 + 56
+    got, want = _device_digests(engine, lens, 0x91)
+    assert np.array_equal(got, want)
+
+
 def test_unknown_policy_rejected(engine):
     rc = engine._lib.msha_set_kernel_policy(engine._ctx, 7)
     assert rc == L.MSHA_ERR_INVALID_ARG
