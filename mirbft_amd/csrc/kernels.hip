@@ -700,6 +700,17 @@ __global__ __launch_bounds__(256, 8) void k_digest_uniform(const uint8_t* __rest
     hash_message<MODE>(p, msg_len, out + 32 * i);
 }
 
+__global__ __launch_bounds__(256) void k_digest_uniform_pipe(const uint8_t* __restrict__ arena,
+                                                             uint64_t stride, uint64_t msg_len,
+                                                             uint64_t n, uint8_t* __restrict__ out,
+                                                             uint32_t* __restrict__ err) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint8_t* p = arena + i * stride;
+  if (check_aligned(p, out + 32 * i, err))
+    hash_message_pipe(p, msg_len, out + 32 * i);
+}
+
 // Digest-of-digests (Batch / VerifyBatch actions, /root/reference/pkg/statemachine/
 // sequence.go:155-158, batch_tracker.go:175-178): out[i] = SHA256(concat over
 // k in [begin[i], begin[i+1]) of table[idx[k]]), every part a 32-byte digest
@@ -753,7 +764,8 @@ static inline void with_mode(int mode, F&& f) {
   switch (mode) {
     case kSingle: f(std::integral_constant<int, kSingle>()); break;
     case kPrefetch:
-    case kPipe:  // the pipelined loop has its own kernel (k_digest_batch_pipe)
+    case kPipe:  // the pipelined loop has its own kernels (k_digest_*_pipe); the
+                 // split kernel never gets kPipe (it runs >= 2 waves per SIMD)
       f(std::integral_constant<int, kPrefetch>()); break;
     default: f(std::integral_constant<int, kPair>()); break;
   }
@@ -819,7 +831,13 @@ hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st) {
   if (n == 0) return hipSuccess;
-  with_mode(pick_mode(n, cus), [&](auto m) {
+  const int mode = pick_mode(n, cus);
+  if (mode == kPipe) {
+    hipLaunchKernelGGL(k_digest_uniform_pipe, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
+                       msg_len, n, out, err);
+    return hipGetLastError();
+  }
+  with_mode(mode, [&](auto m) {
     hipLaunchKernelGGL(k_digest_uniform<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
                        arena, stride, msg_len, n, out, err);
   });

@@ -1,7 +1,8 @@
 """Both batch kernels, forced: one lane per message (MSHA_KERNEL_LANE) and
 cooperative chaining (MSHA_KERNEL_COOP: producer wave expands the schedule
 into LDS, consumer wave runs the rounds). Bit-exact vs the oracle and the
-golden fixtures under each policy; AUTO is covered by test_gpu_parity.py.
+golden fixtures under each policy; AUTO is covered by test_gpu_parity.py,
+plus the pipelined lane kernels' edge cases at the end of this file.
 """
 import hashlib
 
@@ -132,6 +133,20 @@ def _device_digests(engine, lens, salt):
 def test_pipe_uniform_lengths(engine, size):
     got, want = _device_digests(engine, [size] * 40_000, 0x90 + size)
     assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("size,stride", [(0, 16), (56, 64), (128, 128), (183, 192), (1000, 1024)])
+def test_pipe_uniform_kernel(engine, size, stride):
+    """k_digest_uniform_pipe (uniform layout, n in the one-wave-per-SIMD range)."""
+    import torch
+    n = 40_000
+    arena = W.random_bytes(W.SEED ^ 0x92, 8 * size, n * stride + 64)
+    out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_uniform_device(_dev(arena), stride, size, n, out)
+    engine.device_status()
+    off = (np.arange(n, dtype=np.uint64) * stride).astype(np.uint64)
+    want = oracle.digest_batch(arena, off, np.full(n, size, dtype=np.uint64))
+    assert np.array_equal(out.cpu().numpy(), want)
 
 
 def test_pipe_ragged_lengths(engine):
