@@ -771,7 +771,7 @@ static inline void with_mode(int mode, F&& f) {
   }
 }
 
-// Split chaining (AUTO and LANE) when the launch is q >= 2 full rounds of waves
+// Split chaining (AUTO and LANE) when the launch is q >= 1 full rounds of waves
 // over the SIMDs plus a surplus of r <= SIMDs/2 waves: r chains of
 // clamp(SIMDs / r, 2, kMaxSegments) segments, so no SIMD carries more than one
 // segment. MSHA_SPLIT_SEGS overrides the cap for A/B (profiles/r01_ab_segs/).
@@ -780,11 +780,12 @@ constexpr int kMaxSegments = 8;
 bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp) {
   static const int forced = env_int("MSHA_SPLIT", -1);  // A/B: 0 = never
   static const int max_segs = std::min(64, std::max(2, env_int("MSHA_SPLIT_SEGS", kMaxSegments)));
+  static const uint64_t min_q = (uint64_t)std::max(1, env_int("MSHA_SPLIT_MIN_Q", 1));  // A/B
   if (forced == 0 || policy == 2) return false;
   const uint64_t simds = (uint64_t)cus * 4;
   const uint64_t waves = (n + 63) / 64;
   const uint64_t q = waves / simds, r = waves % simds;
-  if (q < 2 || r == 0 || r > simds / 2) return false;
+  if (q < min_q || r == 0 || r > simds / 2) return false;
   sp->n_main = q * simds * 64;
   sp->chains = (uint32_t)r;
   sp->segments = (uint32_t)std::min<uint64_t>(max_segs, std::max<uint64_t>(2, simds / r));

@@ -453,16 +453,17 @@ def _cus():
     return torch.cuda.get_device_properties(0).multi_processor_count
 
 
+@pytest.mark.parametrize("rounds", [1, 2])
 @pytest.mark.parametrize("surplus_waves,tail", [(1, 0), (6, 17), (53, 0), (None, 5)])
-def test_split_chaining_tail(engine, surplus_waves, tail):
-    """Launches of q >= 2 full rounds of waves plus a surplus of 1..SIMDs/2 waves
+def test_split_chaining_tail(engine, rounds, surplus_waves, tail):
+    """Launches of q >= 1 full rounds of waves plus a surplus of 1..SIMDs/2 waves
     run the surplus as split chains (a message's state handed between segment
     waves); every digest bit-exact vs the oracle, with and without a lane order,
     mixed lengths (segments of 0 blocks included), and through the host API."""
     import torch
     simds = _cus() * 4
     r = surplus_waves if surplus_waves is not None else simds // 2    # max surplus
-    n = 2 * simds * 64 + r * 64 - (64 - tail if tail else 0)
+    n = rounds * simds * 64 + r * 64 - (64 - tail if tail else 0)
     rng = np.random.default_rng(r)
     lens = rng.choice(np.array([0, 55, 56, 64, 119, 640, 1000], dtype=np.uint64), size=n)
     offs = np.zeros(n, dtype=np.uint64)
@@ -485,15 +486,16 @@ def test_split_chaining_tail(engine, surplus_waves, tail):
     assert np.array_equal(engine.digest_batch(w.arena, w.off, w.len), exp)
 
 
+@pytest.mark.parametrize("rounds", [1, 2])
 @pytest.mark.parametrize("surplus_waves,tail", [(1, 0), (7, 33), (None, 0)])
-def test_split_chaining_digest_of_digests(engine, surplus_waves, tail):
+def test_split_chaining_digest_of_digests(engine, rounds, surplus_waves, tail):
     """Digest-of-digests launches with a surplus of waves run the surplus as split
     chains; ragged digest counts (0, 1, odd, even, up to 40) so segments start on
     pair blocks, the odd-digest final block and the length-only final block."""
     import torch
     simds = _cus() * 4
     r = surplus_waves if surplus_waves is not None else simds // 2
-    n = 2 * simds * 64 + r * 64 - (64 - tail if tail else 0)
+    n = rounds * simds * 64 + r * 64 - (64 - tail if tail else 0)
     rng = np.random.default_rng(100 + r)
     table = rng.integers(0, 256, size=(4096, 32), dtype=np.uint8)
     cnt = rng.choice(np.array([0, 1, 2, 3, 19, 20, 40], dtype=np.uint64), size=n)
