@@ -19,8 +19,8 @@
  * Conventions
  *  - Every function returns MSHA_OK (0) or a positive MSHA_ERR_* code; nothing
  *    throws or aborts across the ABI. msha_last_error() describes the last
- *    failure on a context (or, for ctx == NULL, the last failure of
- *    msha_ctx_create on this thread).
+ *    failure on a context (or, for ctx == NULL, the last failed context
+ *    creation in the process; msha_ctx_create_err returns it with the call).
  *  - Host pointers are owned by the caller and only used during the call; the
  *    library copies into its own pinned staging and device memory and never
  *    retains them. Digests are written to caller memory (32 bytes each, in input
@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 2u
+#define MSHA_ABI_VERSION 3u
 
 enum {
   MSHA_OK = 0,
@@ -69,11 +69,39 @@ typedef struct {
   uint64_t blocks;         /* 64-byte compressions performed */
   /* Last host-memory call, milliseconds of wall time: */
   double plan_ms;          /* validation, alias detection, sharding, size-class order, placement */
-  double pack_ms;          /* gathering payload bytes into pinned staging (threads) */
+  double pack_ms;          /* gathering payload bytes into pinned staging (summed over shards) */
   double device_ms;        /* first upload .. last kernel on the device (HIP events, max over GPUs) */
   double total_ms;         /* whole call */
   uint64_t direct_calls;   /* host calls whose arena was uploaded as is (pinned, 16-B aligned) */
+  /* Kernel launches by kind, cumulative over every entry point: */
+  uint64_t launches_lane;   /* one lane per message (k_digest_batch / k_digest_uniform) */
+  uint64_t launches_pipe;   /* software-pipelined lane kernel (k_digest_*_pipe), <= 1 wave/SIMD */
+  uint64_t launches_coop;   /* cooperative chaining (k_digest_coop) */
+  uint64_t launches_split;  /* split chaining (k_digest_split, arena or digest-of-digests) */
+  uint64_t launches_dod;    /* digest-of-digests, unsplit (k_digest_of_digests) */
+  uint64_t split_retries;   /* host-call shards whose split launch timed out and were re-run unsplit */
+  /* Last host-memory call, summed over GPUs (see msha_get_shard_stats): */
+  uint64_t h2d_bytes;       /* payload + metadata uploaded */
+  uint64_t d2h_bytes;       /* digests + status words downloaded */
 } msha_stats;
+
+/* Per-GPU figures of the last host-memory call (one entry per shard; a shard is
+ * one GPU, or one virtual shard under MSHA_VIRTUAL_SHARDS). Times are
+ * milliseconds since the call began. */
+typedef struct {
+  int32_t device;              /* HIP device id */
+  uint32_t reserved;
+  uint64_t messages;           /* messages of this shard */
+  uint64_t lanes;              /* distinct payloads hashed (aliases fold) */
+  uint64_t h2d_payload_bytes;  /* message bytes uploaded (compacted byte ranges or staged chunks) */
+  uint64_t h2d_bytes;          /* payload + metadata */
+  uint64_t d2h_bytes;
+  uint64_t launches;           /* kernel launches */
+  double gather_begin_ms;      /* pageable arenas: first / last gather into pinned staging */
+  double gather_end_ms;
+  double gather_ms;            /* time spent gathering (sum over chunks) */
+  double device_ms;            /* first upload .. last kernel (HIP events) */
+} msha_shard_stats;
 
 uint32_t msha_abi_version(void);
 
@@ -83,11 +111,21 @@ int msha_device_count(int* n);
 /* Create a context on the devices in device_mask (bit i = HIP device i);
  * device_mask == 0 means "device 0". Independent actions are sharded across
  * the masked devices (one stream per device, partitioned by cumulative block
- * count); no inter-GPU collective is used. */
+ * count); no inter-GPU collective is used.
+ * On failure the reason is written, NUL-terminated, into errbuf (when errbuf
+ * is not NULL and errbuf_len > 0): the error travels with the call, so a
+ * caller whose thread may change between two calls (a goroutine) still gets it. */
+int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint64_t errbuf_len);
+/* The same; the reason of the most recent failed creation in the PROCESS is
+ * then readable through msha_last_error(NULL) (prefer msha_ctx_create_err when
+ * several threads create contexts). */
 int msha_ctx_create(uint32_t device_mask, msha_ctx** out);
 void msha_ctx_destroy(msha_ctx* ctx);
 const char* msha_last_error(const msha_ctx* ctx);
 int msha_get_stats(const msha_ctx* ctx, msha_stats* out);
+/* Shards of the context (GPUs in device_mask, or virtual shards). */
+int msha_shard_count(const msha_ctx* ctx, uint32_t* n);
+int msha_get_shard_stats(const msha_ctx* ctx, uint32_t shard, msha_shard_stats* out);
 
 /*
  * ProcessHashActions over a packed arena (serial.go:180-198).

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -44,6 +44,31 @@ class MshaStats(ctypes.Structure):
         ("device_ms", ctypes.c_double),
         ("total_ms", ctypes.c_double),
         ("direct_calls", ctypes.c_uint64),
+        ("launches_lane", ctypes.c_uint64),
+        ("launches_pipe", ctypes.c_uint64),
+        ("launches_coop", ctypes.c_uint64),
+        ("launches_split", ctypes.c_uint64),
+        ("launches_dod", ctypes.c_uint64),
+        ("split_retries", ctypes.c_uint64),
+        ("h2d_bytes", ctypes.c_uint64),
+        ("d2h_bytes", ctypes.c_uint64),
+    ]
+
+
+class MshaShardStats(ctypes.Structure):
+    _fields_ = [
+        ("device", ctypes.c_int32),
+        ("reserved", ctypes.c_uint32),
+        ("messages", ctypes.c_uint64),
+        ("lanes", ctypes.c_uint64),
+        ("h2d_payload_bytes", ctypes.c_uint64),
+        ("h2d_bytes", ctypes.c_uint64),
+        ("d2h_bytes", ctypes.c_uint64),
+        ("launches", ctypes.c_uint64),
+        ("gather_begin_ms", ctypes.c_double),
+        ("gather_end_ms", ctypes.c_double),
+        ("gather_ms", ctypes.c_double),
+        ("device_ms", ctypes.c_double),
     ]
 
 
@@ -52,9 +77,13 @@ SIGNATURES = {
     "msha_abi_version": (ctypes.c_uint32, []),
     "msha_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "msha_ctx_create": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_ctxp)]),
+    "msha_ctx_create_err": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_ctxp), ctypes.c_char_p,
+                                           ctypes.c_uint64]),
     "msha_ctx_destroy": (None, [_ctxp]),
     "msha_last_error": (ctypes.c_char_p, [_ctxp]),
     "msha_get_stats": (ctypes.c_int, [_ctxp, ctypes.POINTER(MshaStats)]),
+    "msha_shard_count": (ctypes.c_int, [_ctxp, ctypes.POINTER(ctypes.c_uint32)]),
+    "msha_get_shard_stats": (ctypes.c_int, [_ctxp, ctypes.c_uint32, ctypes.POINTER(MshaShardStats)]),
     "msha_hash_actions": (ctypes.c_int, [_ctxp, _u8p, ctypes.c_uint64, _u64p, _u64p, ctypes.c_uint64,
                                          _u64p, ctypes.c_uint64, _u8p]),
     "msha_digest_batch": (ctypes.c_int, [_ctxp, _u8p, ctypes.c_uint64, _u64p, _u64p, ctypes.c_uint64,

@@ -294,12 +294,18 @@ __global__ __launch_bounds__(256) void k_digest_batch_pipe(const uint8_t* __rest
 // it), so every wait is on a resident or finished wave.
 //
 // A chain's flag word: epoch (bits 63..40) | segments done (39..32) | beat.
-// The running segment stores a new beat every block, so a waiter can tell a
-// long chain (huge messages) from a stuck one: only 100 ms without any
-// change of the word (never expected) raises error bit 2 and unblocks the
-// chain, so every wave exits.
+// The running segment stores a new beat every kBeatBlocks (8) blocks, so a
+// waiter can tell a long chain (huge messages) from a stuck one: only 100 ms
+// without any change of the word (never expected) raises error bit 2 and
+// unblocks the chain, so every wave exits. The host entry points then re-run
+// the launch unsplit (msha_stats.split_retries); the device entry points
+// report MSHA_ERR_HIP through msha_device_status. The clock only runs while
+// the waiter itself runs: a gap of over 1 ms between two of its own polls
+// means the queue was descheduled (time slicing, another process), and the
+// running segment was frozen with it, so the wait restarts.
 // ---------------------------------------------------------------------------
 constexpr uint64_t kSplitWaitTicks = 10000000;  // 100 ms of s_memrealtime (100 MHz)
+constexpr uint64_t kSplitDeschedTicks = 100000;  // 1 ms between two polls: descheduled
 
 __device__ __forceinline__ uint64_t split_word(uint64_t epoch, uint32_t done, uint32_t beat) {
   return ((epoch & 0xFFFFFFu) << 40) | ((uint64_t)(done & 0xFFu) << 32) | beat;
@@ -344,6 +350,7 @@ __device__ __forceinline__ void hash_blocks(State& s, const uint8_t* p, uint64_t
 // first segment also runs the source's checks) and blocks() runs its blocks
 // [b0, b1).
 struct ArenaSrc {  // messages arena[off[m] : off[m]+len[m]] (k_digest_batch's form)
+  static constexpr int kMinWaves = 8;  // occupancy hint (__launch_bounds__): <= 64 VGPRs
   const uint8_t* arena;
   const uint64_t* off;
   const uint64_t* len;
@@ -418,6 +425,10 @@ __device__ __forceinline__ void dod_final_block(const uint4* tab, const uint32_t
 }
 
 struct DigestSrc {
+  // Occupancy hint: the paired digest loads hold a second block (16 VGPRs) while
+  // the first is compressed, ~70 VGPRs. 6 waves per SIMD still hide the loads
+  // (the compression loop's issue rate is flat from 2 to 8 waves).
+  static constexpr int kMinWaves = 6;
   const uint8_t* table;
   const uint32_t* idx;
   const uint64_t* begin;
@@ -431,13 +442,28 @@ struct DigestSrc {
   __device__ __forceinline__ void full(uint64_t i, uint8_t* out) const {
     const uint64_t k0 = begin[i], cnt = begin[i + 1] - k0;
     const uint4* tab = reinterpret_cast<const uint4*>(table);
+    const uint32_t* ix = idx + k0;
     State s;
     state_init(s);
-    uint32_t w[16];
+    uint32_t w[16], nx[16];
     uint64_t k = 0;
-    for (; k + 2 <= cnt; k += 2) {
+    // Two blocks (four digests) per step, all requested before the first is
+    // compressed: with a contiguous idx (the Batch shape) that is both halves
+    // of a 128-byte line back to back, so the line is fetched from HBM once
+    // instead of being evicted between two half-line requests a block apart
+    // (1.57x the algorithmic bytes before, profiles/r01_pmc.json).
+    for (; k + 4 <= cnt; k += 4) {
+      dod_pair_block(tab, ix, k, w);
+      dod_pair_block(tab, ix, k + 2, nx);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(nx[j]));  // keep the second load here
+      compress(s, w);
+      compress(s, nx);
+    }
+    if (k + 2 <= cnt) {
       dod_pair_block(tab, idx + k0, k, w);
       compress(s, w);
+      k += 2;
     }
     // A wave-uniform even count (the Batch shape: BatchSize acks per batch) leaves a
     // final block of padding and length only, the same for every lane: its schedule
@@ -477,7 +503,7 @@ struct DigestSrc {
 };
 
 template <int MODE, class Src>
-__global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, uint8_t* __restrict__ out,
+__global__ __launch_bounds__(256, Src::kMinWaves) void k_digest_split(Src src, uint64_t n, uint8_t* __restrict__ out,
                                                       uint32_t* __restrict__ err, SplitPlan sp) {
   const uint32_t seg_wgs = sp.segments * sp.groups;
   if (blockIdx.x >= seg_wgs) {  // main workgroups: one lane per message, [0, n_main)
@@ -494,12 +520,15 @@ __global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, ui
   const uint64_t ep = split_word(sp.epoch, 0, 0);
   if (seg > 0) {  // wait until seg segments of this chain are done (same launch: same epoch)
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t prev = t0;
     uint64_t seen = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     while ((seen >> 40) != (ep >> 40) || ((seen >> 32) & 0xFF) < seg) {
       __builtin_amdgcn_s_sleep(8);
       const uint64_t now = __builtin_amdgcn_s_memrealtime();
       const uint64_t v = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if (v != seen) {  // the chain moved (a beat or a handoff): restart the clock
+      if (v != seen || now - prev > kSplitDeschedTicks) {
+        // the chain moved (a beat or a handoff), or this wave was descheduled
+        // (and the running segment with it): restart the clock
         seen = v;
         t0 = now;
       } else if (now - t0 > kSplitWaitTicks) {
@@ -510,6 +539,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, ui
         }
         return;
       }
+      prev = now;
     }
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
@@ -538,7 +568,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_split(Src src, uint64_t n, ui
       }
     }
   }
-  if (seg + 1 < sp.segments) {
+  if (seg + 1 < sp.segments && !(seg == 0 && chain == sp.stall_chain)) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     if (lane == 0)
       __hip_atomic_store(flag, split_word(sp.epoch, seg + 1, 0), __ATOMIC_RELAXED,
@@ -716,7 +746,7 @@ __global__ __launch_bounds__(256) void k_digest_uniform_pipe(const uint8_t* __re
 // k in [begin[i], begin[i+1]) of table[idx[k]]), every part a 32-byte digest
 // already resident in HBM (e.g. request digests produced by k_digest_batch).
 // Two digests fill one 64-byte block; the tail block holds 0 or 1 digest.
-__global__ __launch_bounds__(256, 8) void k_digest_of_digests(const uint8_t* __restrict__ table,
+__global__ __launch_bounds__(256, DigestSrc::kMinWaves) void k_digest_of_digests(const uint8_t* __restrict__ table,
                                                            const uint32_t* __restrict__ idx,
                                                            const uint64_t* __restrict__ begin,
                                                            uint64_t n, uint8_t* __restrict__ out) {
@@ -758,17 +788,27 @@ bool uses_coop(uint64_t n, int cus, int policy) {
   return n <= (uint64_t)cus * kCoopMsgsPerWg;
 }
 
-// Calls f(std::integral_constant<int, MODE>) for the runtime mode.
+// Calls f(std::integral_constant<int, MODE>) for a runtime load mode of the
+// templated lane kernels (kSingle / kPrefetch / kPair). kPipe is not one of
+// them: the pipelined loop has kernels of its own (k_digest_*_pipe), and the
+// callers pick those before getting here.
 template <class F>
 static inline void with_mode(int mode, F&& f) {
   switch (mode) {
     case kSingle: f(std::integral_constant<int, kSingle>()); break;
-    case kPrefetch:
-    case kPipe:  // the pipelined loop has its own kernels (k_digest_*_pipe); the
-                 // split kernel never gets kPipe (it runs >= 2 waves per SIMD)
-      f(std::integral_constant<int, kPrefetch>()); break;
+    case kPrefetch: f(std::integral_constant<int, kPrefetch>()); break;
     default: f(std::integral_constant<int, kPair>()); break;
   }
+}
+
+// Load mode of a split launch's main workgroups (q = n_main / (64 SIMDs) full
+// rounds of waves, q >= 1): prefetching below 3 waves per SIMD, paired loads
+// from 3 (the same thresholds as pick_mode, without its kPipe range: the split
+// kernel's segment waves share the SIMDs, so the main waves are never alone).
+static inline int split_mode(const SplitPlan& sp, int cus) {
+  static const int forced = env_int("MSHA_LOAD_MODE", -1);
+  if (forced >= kSingle && forced <= kPair) return forced;
+  return sp.n_main < (uint64_t)cus * 4 * 64 * 3 ? kPrefetch : kPair;
 }
 
 // Split chaining (AUTO and LANE) when the launch is q >= 1 full rounds of waves
@@ -792,71 +832,92 @@ bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp) {
   // 4 chains per 256-thread workgroup; a multiple of 8 workgroups per segment
   // keeps a chain's segments on one XCD (workgroup id mod 8)
   sp->groups = (uint32_t)(((r + 3) / 4 + 7) / 8 * 8);
+  // Failure-path test (tests/test_gpu_failure.py): MSHA_SPLIT_STALL=1 makes chain
+  // 0's first segment skip its handoff, so the waiting segments time out. Read
+  // per launch (not cached) so a test can toggle it in one process.
+  const char* stall = getenv("MSHA_SPLIT_STALL");
+  sp->stall_chain = stall && atoi(stall) == 1 ? 0u : 0xFFFFFFFFu;
   return true;
+}
+
+static inline void set_kind(LaunchKind* kind, LaunchKind k) {
+  if (kind) *kind = k;
 }
 
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
                                const uint32_t* order, const uint32_t* out_idx, uint64_t n,
                                uint8_t* out, uint32_t* err, int cus, int policy, hipStream_t st,
-                               const SplitPlan* split) {
+                               const SplitPlan* split, LaunchKind* kind) {
+  set_kind(kind, kLaunchNone);
   if (n == 0) return hipSuccess;
   if (split) {
     const unsigned grid = split->segments * split->groups + (unsigned)(split->n_main / 256);
     const ArenaSrc src{arena, off, len, order, out_idx, err};
-    with_mode(pick_mode(split->n_main, cus), [&](auto m) {
+    with_mode(split_mode(*split, cus), [&](auto m) {
       hipLaunchKernelGGL((k_digest_split<decltype(m)::value, ArenaSrc>), dim3(grid), dim3(256), 0,
                          st, src, n, out, err, *split);
     });
+    set_kind(kind, kLaunchSplit);
     return hipGetLastError();
   }
   if (uses_coop(n, cus, policy)) {
     const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
     hipLaunchKernelGGL(k_digest_coop<kPrefetch>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len,
                        order, out_idx, n, out, err);
+    set_kind(kind, kLaunchCoop);
     return hipGetLastError();
   }
   const int mode = pick_mode(n, cus);
   if (mode == kPipe) {
     hipLaunchKernelGGL(k_digest_batch_pipe, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
                        order, out_idx, n, out, err);
+    set_kind(kind, kLaunchPipe);
     return hipGetLastError();
   }
   with_mode(mode, [&](auto m) {
     hipLaunchKernelGGL(k_digest_batch<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
                        arena, off, len, order, out_idx, n, out, err);
   });
+  set_kind(kind, kLaunchLane);
   return hipGetLastError();
 }
 
 hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
-                                 hipStream_t st) {
+                                 hipStream_t st, LaunchKind* kind) {
+  set_kind(kind, kLaunchNone);
   if (n == 0) return hipSuccess;
   const int mode = pick_mode(n, cus);
   if (mode == kPipe) {
     hipLaunchKernelGGL(k_digest_uniform_pipe, dim3(grid_for(n)), dim3(256), 0, st, arena, stride,
                        msg_len, n, out, err);
+    set_kind(kind, kLaunchPipe);
     return hipGetLastError();
   }
   with_mode(mode, [&](auto m) {
     hipLaunchKernelGGL(k_digest_uniform<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
                        arena, stride, msg_len, n, out, err);
   });
+  set_kind(kind, kLaunchLane);
   return hipGetLastError();
 }
 
 hipError_t launch_digest_of_digests(const uint8_t* table, const uint32_t* idx,
                                     const uint64_t* begin, uint64_t n, uint8_t* out,
-                                    uint32_t* err, hipStream_t st, const SplitPlan* split) {
+                                    uint32_t* err, hipStream_t st, const SplitPlan* split,
+                                    LaunchKind* kind) {
+  set_kind(kind, kLaunchNone);
   if (n == 0) return hipSuccess;
   if (split) {
     const unsigned grid = split->segments * split->groups + (unsigned)(split->n_main / 256);
     hipLaunchKernelGGL((k_digest_split<0, DigestSrc>), dim3(grid), dim3(256), 0, st,
                        DigestSrc{table, idx, begin}, n, out, err, *split);
+    set_kind(kind, kLaunchSplit);
     return hipGetLastError();
   }
   hipLaunchKernelGGL(k_digest_of_digests, dim3(grid_for(n)), dim3(256), 0, st, table, idx, begin,
                      n, out);
+  set_kind(kind, kLaunchDod);
   return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <functional>
 #include <condition_variable>
@@ -41,7 +42,20 @@ struct MshaError : std::runtime_error {
                       std::string(#expr) + ": " + hipGetErrorString(e_));                    \
   } while (0)
 
-thread_local std::string g_create_error;
+// Reason of the most recent failed context creation in the process
+// (msha_last_error(NULL)). A fixed, always NUL-terminated buffer written under a
+// mutex: a reader on another thread never sees freed memory. msha_ctx_create_err
+// hands the reason back with the call instead (no cross-call state at all).
+std::mutex g_create_mu;
+char g_create_error[512] = "";
+
+void set_create_error(const std::string& msg, char* errbuf, uint64_t errbuf_len) {
+  {
+    std::lock_guard<std::mutex> g(g_create_mu);
+    std::snprintf(g_create_error, sizeof(g_create_error), "%s", msg.c_str());
+  }
+  if (errbuf && errbuf_len) std::snprintf(errbuf, (size_t)std::min<uint64_t>(errbuf_len, 1u << 20), "%s", msg.c_str());
+}
 
 double now_ms() {
   using namespace std::chrono;
@@ -93,6 +107,91 @@ struct PinBuf {
   template <class T> T* as() const { return static_cast<T*>(p); }
 };
 
+// Worker pool for those phases (thread creation would otherwise cost ~0.1 ms
+// per thread per phase): one process-wide pool, plus one per GPU of a
+// multi-GPU context for its gather thread (pageable arenas). run(T, job) calls
+// job(t) for t in [0, T) on the workers and the calling thread, and returns
+// when all are done. One run at a time: a caller that finds the pool busy
+// (another context planning concurrently) runs its tasks on fresh threads.
+class WorkerPool {
+ public:
+  static WorkerPool& get() {
+    static WorkerPool pool(std::min(16u, std::max(1u, std::thread::hardware_concurrency())) - 1);
+    return pool;
+  }
+  explicit WorkerPool(unsigned helpers) {
+    for (unsigned i = 0; i < helpers; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  unsigned size() const { return (unsigned)workers_.size() + 1; }
+  void run(unsigned T, const std::function<void(unsigned)>& job) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock() || workers_.empty()) {
+      std::vector<std::thread> th;
+      for (unsigned t = 1; t < T; ++t) th.emplace_back(job, t);
+      job(0);
+      for (auto& x : th) x.join();
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      job_ = &job;
+      ntasks_ = T;
+      next_ = 0;
+      pending_ = T;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> g(mu_);
+    done_cv_.wait(g, [&] { return pending_ == 0; });
+    job_ = nullptr;
+  }
+  ~WorkerPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& w : workers_) w.join();
+  }
+
+ private:
+  void work() {  // claim and run tasks of the current generation
+    for (;;) {
+      unsigned t;
+      const std::function<void(unsigned)>* job;
+      {
+        std::lock_guard<std::mutex> g(mu_);
+        if (!job_ || next_ >= ntasks_) return;
+        t = next_++;
+        job = job_;
+      }
+      (*job)(t);
+      std::lock_guard<std::mutex> g(mu_);
+      if (--pending_ == 0) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> g(mu_);
+        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_cv_;
+  const std::function<void(unsigned)>* job_ = nullptr;
+  unsigned ntasks_ = 0, next_ = 0, pending_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
 // Per-GPU state: stream, timing events, device buffers, pinned staging.
 struct Device {
   int id = 0;
@@ -108,12 +207,27 @@ struct Device {
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
-  uint64_t direct_lo = 0;         // direct mode: first caller-arena byte uploaded
+  // Direct mode: the byte ranges of the caller's arena this shard's messages
+  // touch, at granule resolution (upload_direct_spans): caller offset o lives
+  // at device offset direct_map[(o - direct_glo) >> direct_gshift] + the
+  // offset inside the granule. Untouched granules are neither uploaded nor
+  // given device memory.
+  uint64_t direct_glo = 0;
+  unsigned direct_gshift = 16;
+  std::vector<uint64_t> direct_map;
+  std::vector<uint8_t> direct_mark;
+  uint64_t direct_remap(uint64_t o) const {
+    const uint64_t r = o - direct_glo;
+    return direct_map[r >> direct_gshift] + (r & ((1ull << direct_gshift) - 1));
+  }
+  msha_shard_stats st{};          // last host call (msha_get_shard_stats)
+  std::unique_ptr<WorkerPool> gather_pool;  // multi-GPU pageable calls: this GPU's gather helpers
   // split chaining (kernels.hip): kSplitRing flag arrays of cus*2 entries,
   // allocated once and zeroed, never reallocated (launches may be in flight)
   uint64_t* split_flags = nullptr;
   uint64_t split_epoch = 0;
   void release() {
+    gather_pool.reset();
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table}) b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
@@ -159,90 +273,6 @@ inline unsigned plan_threads(uint64_t n) {
   const unsigned hw = std::thread::hardware_concurrency();
   return std::max(1u, std::min(16u, hw));
 }
-// Process-wide worker pool for those phases (thread creation would otherwise
-// cost ~0.1 ms per thread per phase). run(T, job) calls job(t) for t in [0, T)
-// on the workers and the calling thread, and returns when all are done. One
-// run at a time: a caller that finds the pool busy (another context planning
-// concurrently) runs its tasks on fresh threads instead.
-class WorkerPool {
- public:
-  static WorkerPool& get() {
-    static WorkerPool pool;
-    return pool;
-  }
-  void run(unsigned T, const std::function<void(unsigned)>& job) {
-    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
-    if (!busy.owns_lock() || workers_.empty()) {
-      std::vector<std::thread> th;
-      for (unsigned t = 1; t < T; ++t) th.emplace_back(job, t);
-      job(0);
-      for (auto& x : th) x.join();
-      return;
-    }
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      job_ = &job;
-      ntasks_ = T;
-      next_ = 0;
-      pending_ = T;
-      ++gen_;
-    }
-    cv_.notify_all();
-    work();
-    std::unique_lock<std::mutex> g(mu_);
-    done_cv_.wait(g, [&] { return pending_ == 0; });
-    job_ = nullptr;
-  }
-  ~WorkerPool() {
-    {
-      std::lock_guard<std::mutex> g(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& w : workers_) w.join();
-  }
-
- private:
-  WorkerPool() {
-    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-    for (unsigned i = 1; i < std::min(16u, hw); ++i) workers_.emplace_back([this] { loop(); });
-  }
-  void work() {  // claim and run tasks of the current generation
-    for (;;) {
-      unsigned t;
-      const std::function<void(unsigned)>* job;
-      {
-        std::lock_guard<std::mutex> g(mu_);
-        if (!job_ || next_ >= ntasks_) return;
-        t = next_++;
-        job = job_;
-      }
-      (*job)(t);
-      std::lock_guard<std::mutex> g(mu_);
-      if (--pending_ == 0) done_cv_.notify_all();
-    }
-  }
-  void loop() {
-    uint64_t seen = 0;
-    for (;;) {
-      {
-        std::unique_lock<std::mutex> g(mu_);
-        cv_.wait(g, [&] { return stop_ || gen_ != seen; });
-        if (stop_) return;
-        seen = gen_;
-      }
-      work();
-    }
-  }
-  std::vector<std::thread> workers_;
-  std::mutex run_mu_, mu_;
-  std::condition_variable cv_, done_cv_;
-  const std::function<void(unsigned)>* job_ = nullptr;
-  unsigned ntasks_ = 0, next_ = 0, pending_ = 0;
-  uint64_t gen_ = 0;
-  bool stop_ = false;
-};
-
 template <class F>
 void parallel_chunks(uint64_t n, unsigned T, F&& f) {
   if (T <= 1) {
@@ -451,19 +481,45 @@ int guarded(msha_ctx* ctx, F&& f) {
   }
 }
 
-// Split [0, n) into nearly equal contiguous pieces and run f(lo, hi) on a few
-// host threads (gathering into pinned staging is host-bandwidth bound).
+// Split [0, n) into nearly equal contiguous pieces and run f(lo, hi) on the
+// threads of `pool` (gathering into pinned staging is host-bandwidth bound).
 template <class F>
-void parallel_ranges(uint64_t n, uint64_t bytes, F&& f) {
-  unsigned hw = std::thread::hardware_concurrency();
-  unsigned t = (unsigned)std::min<uint64_t>({(uint64_t)std::max(1u, std::min(16u, hw)),
-                                             bytes / (4u << 20) + 1, n});
+void parallel_ranges(WorkerPool& pool, uint64_t n, uint64_t bytes, F&& f) {
+  unsigned t = (unsigned)std::min<uint64_t>({(uint64_t)pool.size(), bytes / (4u << 20) + 1, n});
   if (t <= 1) {
     f(0, n);
     return;
   }
   const std::function<void(unsigned)> job = [&](unsigned k) { f(n * k / t, n * (k + 1) / t); };
-  WorkerPool::get().run(t, job);
+  pool.run(t, job);
+}
+
+// Count a kernel launch in the context's counters (atomically: the pageable
+// multi-GPU path launches from one thread per GPU) and in the shard's.
+void count_launch(msha_ctx* ctx, Device* d, msha::LaunchKind kind) {
+  uint64_t* f = nullptr;
+  switch (kind) {
+    case msha::kLaunchLane: f = &ctx->stats.launches_lane; break;
+    case msha::kLaunchPipe: f = &ctx->stats.launches_pipe; break;
+    case msha::kLaunchCoop: f = &ctx->stats.launches_coop; break;
+    case msha::kLaunchSplit: f = &ctx->stats.launches_split; break;
+    case msha::kLaunchDod: f = &ctx->stats.launches_dod; break;
+    default: return;
+  }
+  __atomic_fetch_add(f, 1, __ATOMIC_RELAXED);
+  if (d) d->st.launches++;
+}
+
+// Device entry points: the context's first device, its error word zeroed once.
+void device_prologue(msha_ctx* ctx, void* stream, hipStream_t* st) {
+  if (ctx->devs.empty()) throw MshaError(MSHA_ERR_INVALID_ARG, "context has no device");
+  Device& d = ctx->devs[0];
+  HIPCHK(hipSetDevice(d.id));
+  if (!d.err.p) {  // first device call: a zeroed error word (hipMalloc does not zero)
+    d.err.ensure(4);
+    HIPCHK(hipMemset(d.err.p, 0, 4));
+  }
+  *st = stream ? static_cast<hipStream_t>(stream) : d.stream;
 }
 
 // Is p inside page-locked host memory the GPU can DMA from (hipHostMalloc /
@@ -588,21 +644,29 @@ constexpr uint64_t kChunkBytes = 32ull << 20;
 // payload is copied and hashed once per GPU.
 // t0: when the entry point was called (plan_ms includes its validation).
 // direct (may be null): the caller's arena is pinned host memory whose message
-// starts are 16-byte aligned (msha_pinned_alloc); then each GPU's byte span of
-// it is DMA'd as is (no gather copy, no re-placement) and off/len index into
-// that span.
+// starts are 16-byte aligned (msha_pinned_alloc); upload_direct_spans() has
+// already queued, per GPU, the byte ranges of it that GPU's messages touch
+// (no gather copy), and off indexes the caller's arena.
 struct Direct {
   const uint8_t* arena;
   const uint64_t* off;
-  bool uploaded = false;  // upload_direct_spans() already queued every shard's span
 };
 
-// Direct mode: queue each shard's byte span of the caller's pinned arena for DMA
-// (copy stream) BEFORE the lanes are planned, so PCIe runs while the host builds
-// the alias table, lane order and metadata: a large batch's planning takes about
-// as long as its upload (c5: ~55 ms of planning beside ~65 ms of H2D). The span
-// of a shard is order-independent (min off .. max off+len over its messages),
-// so it is known as soon as the batch is partitioned. bounds: k+1 entries.
+// Direct mode: queue, per shard, the byte ranges of the caller's pinned arena
+// that its messages touch for DMA (copy stream) BEFORE the lanes are planned,
+// so PCIe runs while the host builds the alias table, lane order and metadata
+// (a large batch's planning takes about as long as its upload: c5 ~40 ms beside
+// ~65 ms of H2D). The ranges are found at granule resolution (>= 64 KiB, at
+// most 2^20 granules per shard): one pass marks the granules each message
+// covers; runs of marked granules are uploaded back to back into the device
+// arena, and untouched granules cost neither PCIe nor HBM. A shard's
+// contiguous slice of a request batch is one run (one span, as before); a
+// shard of an EpochChange storm uploads its own slice plus only the granules
+// of the shared payload pool its aliases reference, not everything between
+// (before: every shard uploaded min(off)..max(off+len), which with the pool at
+// the arena's start meant shard s of k uploaded ~(s+1)/k of the whole arena).
+// Uploads go out in device-space chunks of kDirectChunk, one event each, so
+// lane groups whose payloads have landed can start hashing. bounds: k+1 entries.
 void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off,
                          const uint64_t* len, const uint8_t* arena, uint64_t* bounds) {
   const uint32_t k = (uint32_t)ctx->devs.size();
@@ -610,6 +674,8 @@ void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* o
   for (uint32_t s = 0; s < k; ++s) {
     Device& d = ctx->devs[s];
     const uint64_t a = bounds[s], b = bounds[s + 1];
+    d.arena_bytes = 0;
+    d.st.h2d_payload_bytes = 0;
     if (a == b) continue;
     const unsigned T = plan_threads(b - a);
     std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
@@ -617,15 +683,37 @@ void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* o
       uint64_t l = UINT64_MAX, h = 0;  // thread-local: no false sharing on tlo/thi
       for (uint64_t i = a + x; i < a + y; ++i) {
         l = std::min(l, off[i]);
-        h = std::max(h, off[i] + len[i]);
+        h = std::max(h, off[i] + std::max<uint64_t>(len[i], 1));
       }
       tlo[t] = l;
       thi[t] = h;
     });
     const uint64_t lo = *std::min_element(tlo.begin(), tlo.end());
     const uint64_t hi = *std::max_element(thi.begin(), thi.end());
-    d.direct_lo = lo;
-    d.arena_bytes = hi - lo;
+    unsigned gs = 16;
+    while (((hi - (lo & ~((1ull << gs) - 1))) >> gs) >= (1ull << 20)) ++gs;
+    const uint64_t G = 1ull << gs;
+    const uint64_t glo = lo & ~(G - 1);
+    const uint64_t nG = (hi - glo + G - 1) >> gs;
+    d.direct_glo = glo;
+    d.direct_gshift = gs;
+    std::vector<uint8_t>& mark = d.direct_mark;
+    mark.assign(nG, 0);
+    parallel_chunks(b - a, T, [&](unsigned, uint64_t x, uint64_t y) {
+      for (uint64_t i = a + x; i < a + y; ++i) {
+        const uint64_t g0 = (off[i] - glo) >> gs;
+        const uint64_t g1 = (off[i] + std::max<uint64_t>(len[i], 1) - 1 - glo) >> gs;
+        for (uint64_t g = g0; g <= g1; ++g)
+          if (!__atomic_load_n(&mark[g], __ATOMIC_RELAXED)) __atomic_store_n(&mark[g], 1, __ATOMIC_RELAXED);
+      }
+    });
+    d.direct_map.resize(nG);
+    uint64_t dev_bytes = 0;
+    for (uint64_t g = 0; g < nG; ++g) {
+      d.direct_map[g] = mark[g] ? dev_bytes : UINT64_MAX;
+      dev_bytes += mark[g] ? G : 0;
+    }
+    d.arena_bytes = dev_bytes;
     HIPCHK(hipSetDevice(d.id));
     d.arena.ensure(d.arena_bytes + msha::kArenaSlack);
     const uint64_t chunks = std::max<uint64_t>(1, (d.arena_bytes + kDirectChunk - 1) / kDirectChunk);
@@ -634,15 +722,51 @@ void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* o
       HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
       d.span_ev.push_back(e);
     }
-    for (uint64_t c = 0; c < chunks; ++c) {
-      const uint64_t a0 = c * kDirectChunk, a1 = std::min(d.arena_bytes, a0 + kDirectChunk);
-      if (a1 > a0)
-        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + a0, arena + lo + a0, a1 - a0,
-                              hipMemcpyHostToDevice, d.copy_stream));
-      HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+    // runs of marked granules, clipped to [lo, hi), in ascending device order;
+    // event c is recorded once every byte below device offset (c+1)*kDirectChunk is queued
+    uint64_t c = 0, uploaded = 0;
+    for (uint64_t g = 0; g < nG;) {
+      if (!mark[g]) {
+        ++g;
+        continue;
+      }
+      uint64_t g1 = g;
+      while (g1 < nG && mark[g1]) ++g1;
+      const uint64_t h0 = std::max(lo, glo + g * G), h1 = std::min(hi, glo + g1 * G);
+      for (uint64_t pos = h0; pos < h1;) {
+        const uint64_t dev = d.direct_remap(pos);
+        const uint64_t piece = std::min(h1 - pos, (dev / kDirectChunk + 1) * kDirectChunk - dev);
+        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + dev, arena + pos, piece, hipMemcpyHostToDevice,
+                              d.copy_stream));
+        uploaded += piece;
+        pos += piece;
+        for (; c < chunks && (c + 1) * kDirectChunk <= dev + piece; ++c)
+          HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+      }
+      g = g1;
     }
+    for (; c < chunks; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+    d.st.h2d_payload_bytes = uploaded;
   }
-  trace("direct spans queued", t0);
+  trace("direct ranges queued", t0);
+}
+
+// Re-run shard s of a host call in one unsplit launch over all its lanes, after
+// a split-chain handoff timed out (error bit 2: some of its digests are
+// undefined). Its payload and metadata are still on the device. Synchronous.
+void rerun_unsplit(msha_ctx* ctx, Device& d, const Plan& P, uint8_t* d2h_dst) {
+  HIPCHK(hipSetDevice(d.id));
+  HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
+  msha::LaunchKind kind;
+  HIPCHK(msha::launch_digest_batch(d.arena.as<uint8_t>(), d.off.as<uint64_t>(), d.len.as<uint64_t>(),
+                                   nullptr, P.ordered ? d.order.as<uint32_t>() : nullptr, P.lanes,
+                                   d.out.as<uint8_t>(), d.err.as<uint32_t>(), d.cus, ctx->kernel_policy,
+                                   d.stream, nullptr, &kind));
+  count_launch(ctx, &d, kind);
+  HIPCHK(hipMemcpyAsync(d2h_dst, d.out.p, 32 * P.m, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * P.m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  __atomic_fetch_add(&ctx->stats.split_retries, 1, __ATOMIC_RELAXED);
 }
 
 template <class Gather>
@@ -654,14 +778,19 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
   std::vector<uint64_t> bounds(k + 1);
   if (pre_bounds) std::copy(pre_bounds, pre_bounds + k + 1, bounds.begin());
   else partition(len, n, k, bounds.data());
-  double gather_ms = 0;
 
   std::vector<Plan>& plans = ctx->plans;
   plans.resize(k);
-  for (Plan& P : plans) {
+  for (uint32_t s = 0; s < k; ++s) {
+    Plan& P = plans[s];
     P.m = 0;
     P.next = 0;
     P.launched = 0;
+    msha_shard_stats& st = ctx->devs[s].st;
+    const uint64_t payload = direct ? st.h2d_payload_bytes : 0;  // queued by upload_direct_spans
+    st = msha_shard_stats{};
+    st.device = ctx->devs[s].id;
+    st.h2d_payload_bytes = payload;
   }
   // uid -> first shard-local message with that payload (UINT64_MAX = none
   // yet); only needed to find representatives per shard when k > 1
@@ -674,6 +803,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     d.lo = bounds[s];
     d.hi = bounds[s + 1];
     P.m = d.hi - d.lo;
+    d.st.messages = P.m;
     if (P.m == 0) continue;
     const uint64_t* L = len + d.lo;
     // Aliases (same uid) have identical bytes, hence identical digests: only
@@ -714,6 +844,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       touched.clear();
       if (P.lanes == P.m) P.rep.clear();
     }
+    d.st.lanes = P.lanes;
     trace("representatives", t0);
     P.perm.resize(P.lanes);
     if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
@@ -732,36 +863,18 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     // were folded into their representative above), so every lane of chunk c
     // reads bytes uploaded by the end of chunk c.
     uint64_t acc = 0;
-    if (direct) {  // the shard's span of the caller's pinned arena, uploaded as is
+    if (direct) {  // the shard's byte ranges of the caller's pinned arena, uploaded as is
       const unsigned T = plan_threads(P.lanes);
-      uint64_t lo = d.direct_lo, hi = d.direct_lo + d.arena_bytes;
-      if (!direct->uploaded) {
-        std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
-        parallel_chunks(P.lanes, T, [&](unsigned t, uint64_t a, uint64_t b) {
-          uint64_t l = UINT64_MAX, h = 0;  // thread-local: no false sharing on tlo/thi
-          for (uint64_t q = a; q < b; ++q) {
-            const uint32_t i = P.perm[q];
-            l = std::min(l, direct->off[d.lo + i]);
-            h = std::max(h, direct->off[d.lo + i] + L[i]);
-          }
-          tlo[t] = l;
-          thi[t] = h;
-        });
-        lo = *std::min_element(tlo.begin(), tlo.end());
-        hi = *std::max_element(thi.begin(), thi.end());
-      }
       parallel_chunks(P.lanes, T, [&](unsigned, uint64_t a, uint64_t b) {
         for (uint64_t q = a; q < b; ++q) {
           const uint32_t i = P.perm[q];
-          h_off[q] = direct->off[d.lo + i] - lo;
+          h_off[q] = d.direct_remap(direct->off[d.lo + i]);
           h_len[q] = L[i];
         }
       });
-      d.direct_lo = lo;
-      acc = hi - lo;
+      acc = d.arena_bytes;
       P.lane_cut.assign({0, P.lanes});
-      P.cut_chunk.assign(1, 0);
-      if (direct->uploaded) group_lanes_by_span_chunk(P, h_off, h_len, acc);
+      group_lanes_by_span_chunk(P, h_off, h_len, acc);
     } else {
       // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
       // (lane q's payload lands at h_off[q]; payloads are placed in lane order)
@@ -819,8 +932,11 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (P.ordered) d.order.ensure(4 * P.lanes);
     HIPCHK(hipMemcpyAsync(d.off.p, h_off, 8 * P.lanes, hipMemcpyHostToDevice, d.stream));
     HIPCHK(hipMemcpyAsync(d.len.p, h_len, 8 * P.lanes, hipMemcpyHostToDevice, d.stream));
-    if (P.ordered)
+    d.st.h2d_bytes = 16 * P.lanes;
+    if (P.ordered) {
       HIPCHK(hipMemcpyAsync(d.order.p, h_len + P.m, 4 * P.lanes, hipMemcpyHostToDevice, d.stream));
+      d.st.h2d_bytes += 4 * P.lanes;
+    }
     HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
     HIPCHK(hipEventRecord(d.ev0, d.stream));
     HIPCHK(hipEventRecord(d.slot_free[0], d.copy_stream));
@@ -828,70 +944,101 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
   }
   const double t_plan = now_ms();
   trace("planned (metadata H2D queued)", t0);
-  // Issue chunks round-robin over the GPUs so every copy engine stays busy.
-  for (bool more = true; more;) {
-    more = false;
+
+  // Issue chunk P.next of shard s (gather it into a staging slot and upload it,
+  // or, in direct mode, wait for the span chunk completing its payloads), and
+  // launch the kernel over the lanes accumulated since the last launch once
+  // they fill the GPU (2 waves per SIMD) or at the last chunk: hashing runs
+  // ~30x faster than PCIe delivers bytes, so a launch per 32 MiB chunk would
+  // only buy overlap worth a few % while a chunk of large messages (512 x 64
+  // KiB) leaves most SIMDs idle for the whole of its long chains. Returns
+  // whether shard s has chunks left.
+  auto issue_chunk = [&](uint32_t s, WorkerPool& pool) -> bool {
+    Device& d = ctx->devs[s];
+    Plan& P = plans[s];
+    if (P.m == 0 || P.next + 1 >= P.lane_cut.size()) return false;
+    const size_t c = P.next++;
+    const uint64_t q1 = P.lane_cut[c + 1];
+    const uint64_t u0 = P.lane_cut[c], u1 = P.lane_cut[c + 1];
+    const uint64_t* h_off = d.h_meta.as<uint64_t>();  // lane -> arena offset (gather mode)
+    HIPCHK(hipSetDevice(d.id));
+    if (direct) {
+      // the span chunk completing this lane group's payloads (queued up front)
+      HIPCHK(hipStreamWaitEvent(d.stream, d.span_ev[P.cut_chunk[c]], 0));
+    } else {
+      const uint64_t b0 = h_off[u0];
+      const uint64_t b1 = u1 >= P.lanes ? d.arena_bytes : h_off[u1];
+      PinBuf& slot = d.slot[c & 1];
+      HIPCHK(hipEventSynchronize(d.slot_free[c & 1]));  // its previous H2D has drained
+      const double g0 = now_ms();
+      uint8_t* dst = slot.as<uint8_t>();
+      parallel_ranges(pool, u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
+        for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.perm[u], dst + (h_off[u] - b0));
+      });
+      const double g1 = now_ms();
+      if (d.st.gather_begin_ms == 0) d.st.gather_begin_ms = std::max(g0 - t0, 1e-6);
+      d.st.gather_end_ms = g1 - t0;
+      d.st.gather_ms += g1 - g0;
+      if (b1 > b0)
+        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
+                              d.copy_stream));
+      d.st.h2d_payload_bytes += b1 - b0;
+      HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
+      HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
+      HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
+    }
+    const bool last = P.next + 1 >= P.lane_cut.size();
+    const uint64_t fill = (uint64_t)d.cus * 4 * 64 * 2;
+    if (!last && q1 - P.launched < fill) return !last;
+    const uint64_t l0 = P.launched, lanes = q1 - l0;
+    P.launched = q1;
+    // off/len are lane-indexed; out_idx maps lane -> shard-local message
+    // (identity placement: lane q is message q)
+    msha::SplitPlan sp;
+    msha::LaunchKind kind;
+    HIPCHK(msha::launch_digest_batch(
+        d.arena.as<uint8_t>(), d.off.as<uint64_t>() + l0, d.len.as<uint64_t>() + l0, nullptr,
+        P.ordered ? d.order.as<uint32_t>() + l0 : nullptr, lanes,
+        d.out.as<uint8_t>() + (P.ordered ? 0 : 32 * l0), d.err.as<uint32_t>(), d.cus,
+        ctx->kernel_policy, d.stream, split_for(d, lanes, ctx->kernel_policy, sp), &kind));
+    count_launch(ctx, &d, kind);
+    // Identity lanes: these digests are final, bring them back while later
+    // chunks upload and hash (into the caller's buffer itself if it is pinned).
+    if (P.identity()) {
+      HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * l0,
+                            d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost, d.stream));
+      d.st.d2h_bytes += 32 * lanes;
+    }
+    return !last;
+  };
+  if (!direct && k > 1) {
+    // Pageable arenas over several GPUs: one issuing thread per GPU, each with
+    // its own gather helpers, so the host copy for GPU s+1 never waits on GPU
+    // s's staging slot (msha_shard_stats gather_begin/end show the overlap).
+    const unsigned per = std::max(1u, std::min(16u, std::max(1u, std::thread::hardware_concurrency())) / k);
+    std::vector<std::exception_ptr> errs(k);
+    std::vector<std::thread> th;
     for (uint32_t s = 0; s < k; ++s) {
       Device& d = ctx->devs[s];
-      Plan& P = plans[s];
-      if (P.m == 0 || P.next + 1 >= P.lane_cut.size()) continue;
-      more = true;
-      const size_t c = P.next++;
-      const uint64_t q1 = P.lane_cut[c + 1];
-      const uint64_t u0 = P.lane_cut[c], u1 = P.lane_cut[c + 1];
-      const uint64_t* h_off = d.h_meta.as<uint64_t>();  // lane -> arena offset (gather mode)
-      const uint64_t b0 = direct ? 0 : h_off[u0];
-      const uint64_t b1 = direct || u1 >= P.lanes ? d.arena_bytes : h_off[u1];
-      PinBuf& slot = d.slot[c & 1];
-      HIPCHK(hipSetDevice(d.id));
-      if (direct && direct->uploaded) {
-        // the span chunk completing this lane group's payloads (queued up front)
-        HIPCHK(hipStreamWaitEvent(d.stream, d.span_ev[P.cut_chunk[c]], 0));
-      } else if (direct) {
-        if (b1 > b0)
-          HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>(), direct->arena + d.direct_lo, b1 - b0,
-                                hipMemcpyHostToDevice, d.copy_stream));
-      } else {
-        HIPCHK(hipEventSynchronize(d.slot_free[c & 1]));   // its previous H2D has drained
-        const double g0 = now_ms();
-        uint8_t* dst = slot.as<uint8_t>();
-        parallel_ranges(u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
-          for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.perm[u], dst + (h_off[u] - b0));
-        });
-        gather_ms += now_ms() - g0;
-        if (b1 > b0)
-          HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
-                                d.copy_stream));
-      }
-      if (!(direct && direct->uploaded)) {
-        HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
-        HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
-        HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
-      }
-      // Kernels are launched over the lanes accumulated since the last launch
-      // once they fill the GPU (2 waves per SIMD) or at the last chunk: hashing
-      // runs ~30x faster than PCIe delivers bytes, so a launch per 32 MiB chunk
-      // would only buy overlap worth a few % while a chunk of large messages
-      // (512 x 64 KiB) leaves most SIMDs idle for the whole of its long chains.
-      const bool last = P.next + 1 >= P.lane_cut.size();
-      const uint64_t fill = (uint64_t)d.cus * 4 * 64 * 2;
-      if (!last && q1 - P.launched < fill) continue;
-      const uint64_t l0 = P.launched, lanes = q1 - l0;
-      P.launched = q1;
-      // off/len are lane-indexed; out_idx maps lane -> shard-local message
-      // (identity placement: lane q is message q)
-      msha::SplitPlan sp;
-      HIPCHK(msha::launch_digest_batch(
-          d.arena.as<uint8_t>(), d.off.as<uint64_t>() + l0, d.len.as<uint64_t>() + l0, nullptr,
-          P.ordered ? d.order.as<uint32_t>() + l0 : nullptr, lanes,
-          d.out.as<uint8_t>() + (P.ordered ? 0 : 32 * l0), d.err.as<uint32_t>(), d.cus,
-          ctx->kernel_policy, d.stream, split_for(d, lanes, ctx->kernel_policy, sp)));
-      // Identity lanes: these digests are final, bring them back while later
-      // chunks upload and hash (into the caller's buffer itself if it is pinned).
-      if (P.identity())
-        HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * l0,
-                              d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost,
-                              d.stream));
+      if (!d.gather_pool || d.gather_pool->size() != per) d.gather_pool.reset(new WorkerPool(per - 1));
+      th.emplace_back([&, s] {
+        try {
+          while (issue_chunk(s, *ctx->devs[s].gather_pool)) {
+          }
+        } catch (...) {
+          errs[s] = std::current_exception();
+        }
+      });
+    }
+    for (auto& t : th) t.join();
+    for (auto& e : errs)
+      if (e) std::rethrow_exception(e);
+  } else {
+    // One issuing thread, chunks round-robin over the GPUs so every copy
+    // engine stays busy (direct mode only enqueues waits and launches here).
+    for (bool more = true; more;) {
+      more = false;
+      for (uint32_t s = 0; s < k; ++s) more |= issue_chunk(s, WorkerPool::get());
     }
   }
   for (uint32_t s = 0; s < k; ++s) {
@@ -900,27 +1047,45 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (m == 0) continue;
     HIPCHK(hipSetDevice(d.id));
     HIPCHK(hipEventRecord(d.ev1, d.stream));
-    if (!plans[s].identity())
+    if (!plans[s].identity()) {
       HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+      d.st.d2h_bytes += 32 * m;
+    }
     HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
+    d.st.d2h_bytes += 4;
   }
-  double kernel_ms = 0;
+  double kernel_ms = 0, gather_ms = 0;
+  uint64_t h2d = 0, d2h = 0;
   for (uint32_t s = 0; s < k; ++s) {
     Device& d = ctx->devs[s];
-    const uint64_t m = plans[s].m;
+    Plan& P = plans[s];
+    const uint64_t m = P.m;
     if (m == 0) continue;
     HIPCHK(hipSetDevice(d.id));
     HIPCHK(hipStreamSynchronize(d.stream));
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
+    d.st.device_ms = ms;
     kernel_ms = std::max<double>(kernel_ms, ms);
     uint32_t errflag;
     std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
-    if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out");
+    const bool straight = P.identity() && out_pinned;  // identity digests were D2H'd straight into out
+    if (errflag & 2) {
+      // a split chain's handoff timed out: its digests are undefined; the
+      // payload is still on the device, so re-hash the shard unsplit
+      rerun_unsplit(ctx, d, P, straight ? out + 32 * d.lo : d.h_out.as<uint8_t>());
+      d.st.d2h_bytes += 32 * m + 4;
+      std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+      if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out (re-run failed)");
+    }
     if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
-    const std::vector<uint32_t>& rep = plans[s].rep;
+    d.st.h2d_bytes += d.st.h2d_payload_bytes;
+    h2d += d.st.h2d_bytes;
+    d2h += d.st.d2h_bytes;
+    gather_ms += d.st.gather_ms;
+    const std::vector<uint32_t>& rep = P.rep;
     const uint8_t* h = d.h_out.as<uint8_t>();
-    if (plans[s].identity() && out_pinned) continue;  // D2H'd straight into out
+    if (straight) continue;
     parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
       if (rep.empty())
         std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));
@@ -932,6 +1097,8 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
   ctx->stats.plan_ms = t_plan - t0;
   ctx->stats.pack_ms = gather_ms;
   ctx->stats.device_ms = kernel_ms;
+  ctx->stats.h2d_bytes = h2d;
+  ctx->stats.d2h_bytes = d2h;
   ctx->stats.total_ms = now_ms() - t0;
 }
 
@@ -952,18 +1119,25 @@ int msha_device_count(int* n) {
   return MSHA_OK;
 }
 
-int msha_ctx_create(uint32_t device_mask, msha_ctx** out) {
-  if (!out) return MSHA_ERR_INVALID_ARG;
+int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint64_t errbuf_len) {
+  if (errbuf && errbuf_len) errbuf[0] = 0;
+  if (!out) {
+    set_create_error("null out pointer", errbuf, errbuf_len);
+    return MSHA_ERR_INVALID_ARG;
+  }
   *out = nullptr;
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0) {
     (void)hipGetLastError();
-    g_create_error = "no HIP device available (the engine has no CPU fallback)";
+    set_create_error("no HIP device available (the engine has no CPU fallback)", errbuf, errbuf_len);
     return MSHA_ERR_NO_DEVICE;
   }
   if (device_mask == 0) device_mask = 1;
   msha_ctx* ctx = new (std::nothrow) msha_ctx();
-  if (!ctx) return MSHA_ERR_OUT_OF_MEMORY;
+  if (!ctx) {
+    set_create_error("host allocation failed", errbuf, errbuf_len);
+    return MSHA_ERR_OUT_OF_MEMORY;
+  }
   int rc = guarded(ctx, [&] {
     // MSHA_VIRTUAL_SHARDS=k (testing only): a one-device mask is split into k
     // shards on that same GPU, each with its own streams and buffers, so the
@@ -973,33 +1147,40 @@ int msha_ctx_create(uint32_t device_mask, msha_ctx** out) {
     if ((device_mask & (device_mask - 1)) != 0) virt = 1;
     for (int i = 0; i < 32; ++i) {
       if (!(device_mask & (1u << i))) continue;
-      if (i >= count) throw MshaError(MSHA_ERR_NO_DEVICE, "device_mask names device " + std::to_string(i) + " but only " + std::to_string(count) + " visible");
+      if (i >= count)
+        throw MshaError(MSHA_ERR_NO_DEVICE, "device_mask names device " + std::to_string(i) + " but only " +
+                                                std::to_string(count) + " visible");
       for (int v = 0; v < virt; ++v) {
-      Device d;
-      d.id = i;
-      HIPCHK(hipSetDevice(i));
-      hipDeviceProp_t prop;
-      HIPCHK(hipGetDeviceProperties(&prop, i));
-      d.cus = prop.multiProcessorCount;
-      HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
-      HIPCHK(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
-      HIPCHK(hipEventCreate(&d.ev0));
-      HIPCHK(hipEventCreate(&d.ev1));
-      HIPCHK(hipEventCreateWithFlags(&d.slot_free[0], hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&d.slot_free[1], hipEventDisableTiming));
-      HIPCHK(hipEventCreateWithFlags(&d.chunk_in, hipEventDisableTiming));
-      ctx->devs.push_back(d);
+        Device d;
+        d.id = i;
+        HIPCHK(hipSetDevice(i));
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, i));
+        d.cus = prop.multiProcessorCount;
+        HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreate(&d.ev0));
+        HIPCHK(hipEventCreate(&d.ev1));
+        HIPCHK(hipEventCreateWithFlags(&d.slot_free[0], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.slot_free[1], hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.chunk_in, hipEventDisableTiming));
+        d.st.device = i;
+        ctx->devs.push_back(std::move(d));
       }
     }
   });
   if (rc != MSHA_OK) {
-    g_create_error = ctx->err;
+    set_create_error(ctx->err, errbuf, errbuf_len);
     for (auto& d : ctx->devs) d.release();
     delete ctx;
     return rc;
   }
   *out = ctx;
   return MSHA_OK;
+}
+
+int msha_ctx_create(uint32_t device_mask, msha_ctx** out) {
+  return msha_ctx_create_err(device_mask, out, nullptr, 0);
 }
 
 void msha_ctx_destroy(msha_ctx* ctx) {
@@ -1013,13 +1194,23 @@ void msha_ctx_destroy(msha_ctx* ctx) {
   delete ctx;
 }
 
-const char* msha_last_error(const msha_ctx* ctx) {
-  return ctx ? ctx->err.c_str() : g_create_error.c_str();
-}
+const char* msha_last_error(const msha_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error; }
 
 int msha_get_stats(const msha_ctx* ctx, msha_stats* out) {
   if (!ctx || !out) return MSHA_ERR_INVALID_ARG;
   *out = ctx->stats;
+  return MSHA_OK;
+}
+
+int msha_shard_count(const msha_ctx* ctx, uint32_t* n) {
+  if (!ctx || !n) return MSHA_ERR_INVALID_ARG;
+  *n = (uint32_t)ctx->devs.size();
+  return MSHA_OK;
+}
+
+int msha_get_shard_stats(const msha_ctx* ctx, uint32_t shard, msha_shard_stats* out) {
+  if (!ctx || !out || shard >= ctx->devs.size()) return MSHA_ERR_INVALID_ARG;
+  *out = ctx->devs[shard].st;
   return MSHA_OK;
 }
 
@@ -1097,10 +1288,7 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
                         is_pinned_host(arena + lo);
     Direct dir{arena, off};
     std::vector<uint64_t> bounds(ctx->devs.size() + 1);
-    if (direct) {
-      upload_direct_spans(ctx, t0, n, off, len, arena, bounds.data());
-      dir.uploaded = true;
-    }
+    if (direct) upload_direct_spans(ctx, t0, n, off, len, arena, bounds.data());
     if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table, ctx->alias_bucket, ctx->alias_tag);
     trace("aliases", t0);
     run_pipeline(ctx, t0, n, len, aliases ? ctx->uid.data() : nullptr, out,
@@ -1175,6 +1363,9 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
       const uint64_t lo = bounds[s], hi = bounds[s + 1], m = hi - lo;
       d.lo = lo;
       d.hi = hi;
+      d.st = msha_shard_stats{};
+      d.st.device = d.id;
+      d.st.messages = d.st.lanes = m;
       if (m == 0) continue;
       const uint64_t i0 = begin[lo], i1 = begin[hi];
       HIPCHK(hipSetDevice(d.id));
@@ -1191,17 +1382,23 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
       d.err.ensure(4);
       HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
       HIPCHK(hipEventRecord(d.ev0, d.stream));
+      d.st.h2d_payload_bytes = 32 * n_table;
+      d.st.h2d_bytes = 32 * n_table + 4 * (i1 - i0) + 8 * (m + 1);
       msha::SplitPlan sp;
+      msha::LaunchKind kind;
       HIPCHK(msha::launch_digest_of_digests(d.table.as<uint8_t>(), d.idx.as<uint32_t>(),
                                             d.begin.as<uint64_t>(), m, d.out.as<uint8_t>(),
                                             d.err.as<uint32_t>(), d.stream,
-                                            split_for(d, m, ctx->kernel_policy, sp)));
+                                            split_for(d, m, ctx->kernel_policy, sp), &kind));
+      count_launch(ctx, &d, kind);
       HIPCHK(hipEventRecord(d.ev1, d.stream));
       d.h_out.ensure(32 * m + 4);
       HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
       HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
+      d.st.d2h_bytes = 32 * m + 4;
     }
     double kernel_ms = 0;
+    uint64_t h2d = 0, d2h = 0;
     for (uint32_t s = 0; s < k; ++s) {
       Device& d = ctx->devs[s];
       const uint64_t m = d.hi - d.lo;
@@ -1210,11 +1407,27 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
       HIPCHK(hipStreamSynchronize(d.stream));
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
+      d.st.device_ms = ms;
       kernel_ms = std::max<double>(kernel_ms, ms);
       uint32_t errflag;
       std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
-      if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out");
+      if (errflag & 2) {
+        // a split chain's handoff timed out (its digests are undefined): the
+        // inputs are still on the device, re-hash the shard unsplit
+        HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
+        msha::LaunchKind kind;
+        HIPCHK(msha::launch_digest_of_digests(d.table.as<uint8_t>(), d.idx.as<uint32_t>(),
+                                              d.begin.as<uint64_t>(), m, d.out.as<uint8_t>(),
+                                              d.err.as<uint32_t>(), d.stream, nullptr, &kind));
+        count_launch(ctx, &d, kind);
+        HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+        HIPCHK(hipStreamSynchronize(d.stream));
+        d.st.d2h_bytes += 32 * m;
+        ctx->stats.split_retries++;
+      }
       std::memcpy(out + 32 * d.lo, d.h_out.p, 32 * m);
+      h2d += d.st.h2d_bytes;
+      d2h += d.st.d2h_bytes;
     }
     uint64_t blocks = 0;
     for (uint64_t i = 0; i < n; ++i) blocks += blocks_for(alen[i]);
@@ -1225,20 +1438,10 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
     ctx->stats.plan_ms = 0;
     ctx->stats.pack_ms = 0;
     ctx->stats.device_ms = kernel_ms;
+    ctx->stats.h2d_bytes = h2d;
+    ctx->stats.d2h_bytes = d2h;
     ctx->stats.total_ms = now_ms() - t0;
   });
-}
-
-static int device_prologue(msha_ctx* ctx, void* stream, hipStream_t* st) {
-  if (!ctx || ctx->devs.empty()) return MSHA_ERR_INVALID_ARG;
-  Device& d = ctx->devs[0];
-  HIPCHK(hipSetDevice(d.id));
-  if (!d.err.p) {  // first device call: a zeroed error word (hipMalloc does not zero)
-    d.err.ensure(4);
-    HIPCHK(hipMemset(d.err.p, 0, 4));
-  }
-  *st = stream ? static_cast<hipStream_t>(stream) : d.stream;
-  return MSHA_OK;
 }
 
 int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
@@ -1252,9 +1455,11 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
     device_prologue(ctx, stream, &st);
     Device& d = ctx->devs[0];
     msha::SplitPlan sp;
+    msha::LaunchKind kind;
     HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, d_order, nullptr, n, d_out,
                                      d.err.as<uint32_t>(), d.cus, ctx->kernel_policy, st,
-                                     split_for(d, n, ctx->kernel_policy, sp)));
+                                     split_for(d, n, ctx->kernel_policy, sp), &kind));
+    count_launch(ctx, nullptr, kind);
   });
 }
 
@@ -1268,7 +1473,10 @@ int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t s
     hipStream_t st;
     device_prologue(ctx, stream, &st);
     Device& d = ctx->devs[0];
-    HIPCHK(msha::launch_digest_uniform(d_arena, stride, msg_len, n, d_out, d.err.as<uint32_t>(), d.cus, st));
+    msha::LaunchKind kind;
+    HIPCHK(msha::launch_digest_uniform(d_arena, stride, msg_len, n, d_out, d.err.as<uint32_t>(), d.cus, st,
+                                       &kind));
+    count_launch(ctx, nullptr, kind);
   });
 }
 
@@ -1282,8 +1490,10 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
     device_prologue(ctx, stream, &st);
     Device& d = ctx->devs[0];
     msha::SplitPlan sp;
+    msha::LaunchKind kind;
     HIPCHK(msha::launch_digest_of_digests(d_table, d_idx, d_begin, n, d_out, d.err.as<uint32_t>(), st,
-                                          split_for(d, n, ctx->kernel_policy, sp)));
+                                          split_for(d, n, ctx->kernel_policy, sp), &kind));
+    count_launch(ctx, nullptr, kind);
   });
 }
 

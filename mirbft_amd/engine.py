@@ -65,9 +65,10 @@ class Engine:
     def __init__(self, device_mask: int = 1):
         self._lib = L.lib()
         ctx = ctypes.c_void_p()
-        rc = self._lib.msha_ctx_create(device_mask, ctypes.byref(ctx))
+        err = ctypes.create_string_buffer(512)
+        rc = self._lib.msha_ctx_create_err(device_mask, ctypes.byref(ctx), err, len(err))
         if rc != L.MSHA_OK:
-            raise MshaError(rc, self._lib.msha_last_error(None).decode())
+            raise MshaError(rc, err.value.decode())
         self._ctx = ctx
 
     # -- lifecycle -------------------------------------------------------
@@ -116,6 +117,17 @@ class Engine:
         s = L.MshaStats()
         self._check(self._lib.msha_get_stats(self._ctx, ctypes.byref(s)))
         return {name: getattr(s, name) for name, _ in L.MshaStats._fields_}
+
+    def shard_stats(self) -> list[dict]:
+        """Per-GPU (per-shard) figures of the last host-memory call."""
+        n = ctypes.c_uint32(0)
+        self._check(self._lib.msha_shard_count(self._ctx, ctypes.byref(n)))
+        out = []
+        for i in range(n.value):
+            s = L.MshaShardStats()
+            self._check(self._lib.msha_get_shard_stats(self._ctx, i, ctypes.byref(s)))
+            out.append({name: getattr(s, name) for name, _ in L.MshaShardStats._fields_ if name != "reserved"})
+        return out
 
     # -- host-memory entry points -----------------------------------------
     def digest_batch(self, arena: np.ndarray, off: np.ndarray, length: np.ndarray,

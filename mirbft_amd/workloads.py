@@ -17,6 +17,7 @@ Configs (BASELINE.json "configs"):
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Optional
 
@@ -37,19 +38,30 @@ def splitmix64(seed: int, start: int, count: int) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
-def random_bytes(seed: int, offset: int, nbytes: int, chunk: int = 1 << 24) -> np.ndarray:
-    """Bytes [offset, offset+nbytes) of the splitmix64 byte stream (offset % 8 == 0)."""
+def random_bytes(seed: int, offset: int, nbytes: int, chunk: int = 1 << 22) -> np.ndarray:
+    """Bytes [offset, offset+nbytes) of the splitmix64 byte stream (offset % 8 == 0).
+    Chunks are generated on a few threads (numpy releases the GIL): the full-size
+    configs need GBs of payload (c4: 4.3 GB)."""
     assert offset % 8 == 0
     out = np.empty(nbytes, dtype=np.uint8)
     w0 = offset // 8
     nwords = (nbytes + 7) // 8
-    pos = 0
-    for s in range(0, nwords, chunk):
+
+    def fill(s: int) -> None:
         c = min(chunk, nwords - s)
         b = splitmix64(seed, w0 + s, c).view(np.uint8)
+        pos = 8 * s
         take = min(8 * c, nbytes - pos)
         out[pos:pos + take] = b[:take]
-        pos += take
+
+    starts = range(0, nwords, chunk)
+    if nwords <= chunk:
+        for s in starts:
+            fill(s)
+        return out
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+        list(ex.map(fill, starts))
     return out
 
 

@@ -29,7 +29,7 @@ def test_exports_via_nm():
 
 
 def test_abi_version():
-    assert L.lib().msha_abi_version() == L.ABI_VERSION == 2
+    assert L.lib().msha_abi_version() == L.ABI_VERSION == 3
 
 
 def test_library_is_gfx950_code_object():
@@ -105,3 +105,47 @@ def test_order_by_blocks_threaded_matches_stable_argsort(n, maxlen):
     blocks = (lens >> 6) + np.where((lens & 63) < 56, 1, 2)
     exp = np.argsort(-blocks.astype(np.int64), kind="stable")
     assert np.array_equal(order_by_blocks(lens).astype(np.int64), exp)
+
+
+def test_create_error_travels_with_the_call_and_across_threads():
+    """msha_ctx_create_err writes the reason into the caller's buffer; the
+    process-wide msha_last_error(NULL) is readable from ANOTHER thread (a Go
+    caller's goroutine may resume on a different OS thread between two cgo calls)."""
+    import threading
+    n = ctypes.c_int(-1)
+    L.lib().msha_device_count(ctypes.byref(n))
+    lib = L.lib()
+    ctx = ctypes.c_void_p()
+    mask = 1 << 31 if n.value > 0 else 1      # device 31 does not exist; no device at all on CPU
+    exp_code = L.MSHA_ERR_NO_DEVICE
+    res = {}
+
+    def create():
+        buf = ctypes.create_string_buffer(256)
+        res["rc"] = lib.msha_ctx_create_err(mask, ctypes.byref(ctx), buf, len(buf))
+        res["buf"] = buf.value.decode()
+
+    t = threading.Thread(target=create)
+    t.start()
+    t.join()
+    assert res["rc"] == exp_code and ctx.value is None
+    assert res["buf"], "error text returned with the call"
+    seen = {}
+    t2 = threading.Thread(target=lambda: seen.update(msg=lib.msha_last_error(None).decode()))
+    t2.start()
+    t2.join()
+    assert seen["msg"] == res["buf"]
+    # a tiny buffer is NUL-terminated, truncated, never overrun
+    small = ctypes.create_string_buffer(b"\xff" * 8, 8)
+    assert lib.msha_ctx_create_err(mask, ctypes.byref(ctx), small, 4) == exp_code
+    assert small.raw[3] == 0 and small.raw[4:] == b"\xff" * 4
+    assert lib.msha_ctx_create_err(mask, None, None, 0) == L.MSHA_ERR_INVALID_ARG
+
+
+def test_stats_and_shard_stats_null_args():
+    lib = L.lib()
+    n = ctypes.c_uint32(0)
+    assert lib.msha_shard_count(None, ctypes.byref(n)) == L.MSHA_ERR_INVALID_ARG
+    assert lib.msha_get_shard_stats(None, 0, None) == L.MSHA_ERR_INVALID_ARG
+    assert ctypes.sizeof(L.MshaShardStats) == 8 * 11
+    assert ctypes.sizeof(L.MshaStats) == 8 * 17

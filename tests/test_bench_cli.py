@@ -1,0 +1,53 @@
+"""bench.py's process contract, on CPU: --gpus N drives N rank processes (it
+starts torchrun itself when no WORLD_SIZE is set, before touching a GPU), and
+refuses a WORLD_SIZE that disagrees with --gpus."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_world_size_mismatch_is_an_error():
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in (r.stderr + r.stdout)
+
+
+def test_gpus_n_spawns_n_ranks(monkeypatch):
+    sys.path.insert(0, ROOT)
+    import bench
+    seen = {}
+
+    class R:
+        returncode = 0
+
+    def fake_run(cmd, *a, **k):
+        seen["cmd"] = cmd
+        return R()
+
+    monkeypatch.setattr(subprocess, "run", fake_run)
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "4", "--steps", "3"])
+    args = bench.parse()
+    assert bench.launch_ranks(args) == 0
+    cmd = seen["cmd"]
+    assert cmd[1:3] == ["-m", "torch.distributed.run"] and "--nproc-per-node=4" in cmd
+    assert "127.0.0.1" in cmd and cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+
+
+def test_verify_sample_hits_every_lane_position():
+    sys.path.insert(0, ROOT)
+    import numpy as np
+    import bench
+    from mirbft_amd import workloads as W
+    from oracle import oracle
+    w = W.c2_requests(n=65536)
+    out = oracle.openssl_digest_batch(w.arena, w.off, w.len, 4)
+    bench.verify_sample(w, out)                     # passes on correct digests
+    bad = out.copy()
+    bad[65535, 0] ^= 1                              # the last digest is always sampled
+    with pytest.raises(SystemExit):
+        bench.verify_sample(w, bad)

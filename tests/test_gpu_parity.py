@@ -261,21 +261,53 @@ def test_c3_full_size_bit_exact(engine):
     assert np.array_equal(out2.cpu().numpy(), exp)
 
 
-def test_c4_full_size_sampled(engine):
-    """BASELINE config c4 (65,536 x 64 KiB) on the GPU; 1,024 evenly spaced
-    messages checked against the oracle, plus a digest-of-all-digests check
-    against the same sample set recomputed through the host path."""
+def _oracle_threaded(w, threads: int = 16):
+    """Every digest of a full-size workload: the OpenSSL leg of the oracle over
+    `threads` threads, each distinct (off, len) payload hashed once."""
+    key = (w.off << np.uint64(24)) | w.len          # off < 2^40, len < 2^24 in these configs
+    assert int(w.off.max()) < (1 << 40) and int(w.len.max()) < (1 << 24)
+    uniq, first, inv = np.unique(key, return_index=True, return_inverse=True)
+    d = oracle.openssl_digest_batch(w.arena, w.off[first], w.len[first], threads)
+    return d[inv.reshape(-1)]
+
+
+def test_c4_full_size_bit_exact(engine):
+    """BASELINE config c4 (65,536 x 64 KiB) at full size, every digest vs the oracle,
+    through BOTH kernels that run it: the off/len pipelined lane kernel
+    (k_digest_batch_pipe, the one bench.py times) and the uniform-layout one."""
     import torch
     w = W.c4_large()
+    exp = _oracle_threaded(w)
     d_arena, d_off, d_len = _to_dev(w)
     out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    before = engine.stats()
+    engine.digest_batch_device(d_arena, d_off, d_len, out)
+    engine.device_status()
+    assert engine.stats()["launches_pipe"] == before["launches_pipe"] + 1   # the timed kernel ran
+    assert np.array_equal(out.cpu().numpy(), exp)
+    out.zero_()
     engine.digest_uniform_device(d_arena, w.uniform_stride, 65536, w.n, out)
     engine.device_status()
-    got = out.cpu().numpy()
-    sample = np.arange(0, w.n, 64)
-    exp = oracle.digest_batch(w.arena, w.off[sample], w.len[sample])
-    assert np.array_equal(got[sample], exp)
-    del d_arena
+    assert np.array_equal(out.cpu().numpy(), exp)
+    del d_arena, d_off, d_len, out
+    torch.cuda.empty_cache()
+
+
+def test_c5_full_size_ordered_device(engine):
+    """BASELINE config c5 at its full 2^23 actions on one GPU, through the ordered
+    device path bench.py times (size-class order, aliased EpochChange payloads):
+    every digest vs the oracle."""
+    import torch
+    from mirbft_amd.engine import order_by_blocks
+    w = W.c5_storm()
+    exp = _oracle_threaded(w)
+    d_arena, d_off, d_len = _to_dev(w)
+    d_order = torch.from_numpy(order_by_blocks(w.len).view(np.int32)).to("cuda:0")
+    out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device(d_arena, d_off, d_len, out, order=d_order)
+    engine.device_status()
+    assert np.array_equal(out.cpu().numpy(), exp)
+    del d_arena, d_off, d_len, d_order, out
     torch.cuda.empty_cache()
 
 
@@ -473,6 +505,7 @@ def test_split_chaining_tail(engine, rounds, surplus_waves, tail):
     exp = oracle.digest_batch(w.arena, w.off, w.len)
     d_arena, d_off, d_len = _to_dev(w)
     out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    split0 = engine.stats()["launches_split"]
     engine.digest_batch_device(d_arena, d_off, d_len, out)
     engine.device_status()
     assert np.array_equal(out.cpu().numpy(), exp)
@@ -482,6 +515,7 @@ def test_split_chaining_tail(engine, rounds, surplus_waves, tail):
     engine.digest_batch_device(d_arena, d_off, d_len, out, order=d_order)
     engine.device_status()
     assert np.array_equal(out.cpu().numpy(), exp)
+    assert engine.stats()["launches_split"] == split0 + 2     # both launches were split chains
     # host API (lane-indexed metadata + out_idx through the pipeline)
     assert np.array_equal(engine.digest_batch(w.arena, w.off, w.len), exp)
 
@@ -504,10 +538,12 @@ def test_split_chaining_digest_of_digests(engine, rounds, surplus_waves, tail):
     idx = rng.integers(0, table.shape[0], size=int(begin[-1]), dtype=np.uint32)
     exp = oracle.digest_of_digests(table, idx, begin)
     out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    split0 = engine.stats()["launches_split"]
     engine.digest_of_digests_device(torch.from_numpy(table).to("cuda:0"),
                                     torch.from_numpy(idx.view(np.int32)).to("cuda:0"),
                                     torch.from_numpy(begin.view(np.int64)).to("cuda:0"), out)
     engine.device_status()
+    assert engine.stats()["launches_split"] == split0 + 1
     assert np.array_equal(out.cpu().numpy(), exp)
     assert np.array_equal(engine.digest_of_digests(table, idx, begin), exp)
 
@@ -557,3 +593,44 @@ def test_split_chaining_long_surplus_message(engine):
     engine.digest_batch_device(d_arena, d_off, d_len, out)
     engine.device_status()
     assert np.array_equal(out.cpu().numpy(), exp)
+
+
+def test_direct_upload_compacted_ranges_sharded(monkeypatch):
+    """Direct (pinned) uploads over 4 virtual shards of a c5 batch whose aliased
+    EpochChange pool sits at the arena's start: each shard uploads its own slice
+    plus only the pool granules its aliases touch (before: every shard's span
+    started at offset 0, ~2.5x the arena in total at 4 shards)."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", "4")
+    w = W.c5_storm(1 << 18)
+    own = w.len != 0
+    pool_bytes = int((w.off + w.len)[w.len > 4096].max())          # EpochChange payloads: the pool
+    with Engine(1) as e:
+        pinned = e.pinned_empty(w.arena.size)
+        pinned[:] = w.arena
+        got = e.digest_batch(pinned, w.off, w.len)
+        assert np.array_equal(got, _oracle_dedup(w))
+        sh = e.shard_stats()
+        assert len(sh) == 4 and e.stats()["direct_calls"] == 1
+        payload = sum(s["h2d_payload_bytes"] for s in sh)
+        granule_slack = 4 * 2 * 65536
+        assert payload <= w.arena.size + 3 * pool_bytes + granule_slack, (payload, w.arena.size, pool_bytes)
+        assert e.stats()["h2d_bytes"] == sum(s["h2d_bytes"] for s in sh)
+        assert sum(s["messages"] for s in sh) == w.n and own.any()
+
+
+def test_pageable_gather_runs_per_shard_in_parallel(monkeypatch):
+    """Pageable arenas over 2 shards: one gather/issue thread per GPU, so the
+    host copies for the two shards overlap in time instead of alternating on
+    one thread (msha_shard_stats gather windows)."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", "2")
+    w = W.c2_requests(1 << 20)                  # 512 MiB: 8 staging chunks per shard
+    with Engine(1) as e:
+        got = e.digest_batch(w.arena, w.off, w.len)
+        assert np.array_equal(got, oracle.digest_batch(w.arena, w.off, w.len))
+        sh = e.shard_stats()
+        assert all(s["gather_ms"] > 0 for s in sh)
+        assert max(s["gather_begin_ms"] for s in sh) < min(s["gather_end_ms"] for s in sh), sh
+        assert sum(s["h2d_payload_bytes"] for s in sh) == int(w.len.sum())
+        assert sum(s["launches"] for s in sh) >= 2

@@ -22,8 +22,10 @@ POLICIES = ["lane", "coop"]
 @pytest.fixture(params=POLICIES)
 def eng(request, engine):
     engine.set_kernel_policy(request.param)
+    engine._policy = request.param
     yield engine
     engine.set_kernel_policy("auto")
+    engine._policy = "auto"
 
 
 def _dev(a, dtype=None):
@@ -67,9 +69,21 @@ def test_device_unordered_mixed_blocks(eng):
     off = np.concatenate([[0], np.cumsum(stride)[:-1]]).astype(np.uint64)
     arena = W.random_bytes(W.SEED ^ 0x72, 0, int(stride.sum()) + 64)
     out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    st0 = eng.stats()
     eng.digest_batch_device(_dev(arena), _dev(off), _dev(lens), out)
     eng.device_status()
     assert np.array_equal(out.cpu().numpy(), oracle.digest_batch(arena, off, lens))
+    _assert_policy_kernel(eng, st0)
+
+
+def _assert_policy_kernel(eng, st0):
+    """The forced policy's kernel is the one that ran (msha_stats launch counters)."""
+    st1 = eng.stats()
+    ran = {k: st1[k] - st0[k] for k in ("launches_lane", "launches_pipe", "launches_coop", "launches_split")}
+    if eng._policy == "coop":
+        assert ran == {"launches_lane": 0, "launches_pipe": 0, "launches_coop": 1, "launches_split": 0}, ran
+    else:   # one lane per message: the plain or the pipelined lane kernel
+        assert ran["launches_coop"] == 0 and ran["launches_lane"] + ran["launches_pipe"] + ran["launches_split"] == 1, ran
 
 
 @pytest.mark.parametrize("n", [1 << 14, 40_000])   # coop: latency form (G=2) / balanced form (G=4)
@@ -79,9 +93,11 @@ def test_device_ordered_c5(eng, n):
     w = W.c5_storm(n)
     out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
     order = _dev(order_by_blocks(w.len).view(np.int32))
+    st0 = eng.stats()
     eng.digest_batch_device(_dev(w.arena), _dev(w.off), _dev(w.len), out, order=order)
     eng.device_status()
     assert np.array_equal(out.cpu().numpy(), oracle.digest_batch(w.arena, w.off, w.len))
+    _assert_policy_kernel(eng, st0)
 
 
 def test_partial_last_group(eng):
@@ -114,15 +130,17 @@ def test_large_messages(eng):
     assert eng.hash_actions([[m] for m in msgs]) == [hashlib.sha256(m).digest() for m in msgs]
 
 
-def _device_digests(engine, lens, salt):
+def _device_digests(engine, lens, salt, kernel="launches_pipe"):
     import torch
     lens = np.asarray(lens, dtype=np.uint64)
     stride = (lens + 15) // 16 * 16
     off = np.concatenate([[0], np.cumsum(stride)[:-1]]).astype(np.uint64)
     arena = W.random_bytes(W.SEED ^ salt, 0, int(stride.sum()) + 64)
     out = torch.empty((len(lens), 32), dtype=torch.uint8, device="cuda:0")
+    before = engine.stats()[kernel]
     engine.digest_batch_device(_dev(arena), _dev(off), _dev(lens), out)
     engine.device_status()
+    assert engine.stats()[kernel] == before + 1, f"{kernel} did not run"
     return out.cpu().numpy(), oracle.digest_batch(arena, off, lens)
 
 
@@ -142,8 +160,10 @@ def test_pipe_uniform_kernel(engine, size, stride):
     n = 40_000
     arena = W.random_bytes(W.SEED ^ 0x92, 8 * size, n * stride + 64)
     out = torch.empty((n, 32), dtype=torch.uint8, device="cuda:0")
+    before = engine.stats()["launches_pipe"]
     engine.digest_uniform_device(_dev(arena), stride, size, n, out)
     engine.device_status()
+    assert engine.stats()["launches_pipe"] == before + 1      # the uniform pipelined kernel ran
     off = (np.arange(n, dtype=np.uint64) * stride).astype(np.uint64)
     want = oracle.digest_batch(arena, off, np.full(n, size, dtype=np.uint64))
     assert np.array_equal(out.cpu().numpy(), want)

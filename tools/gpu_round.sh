@@ -7,7 +7,7 @@ export TMPDIR=/tmp
 stop_on_fault() { local rc=$1 name=$2; echo "$name rc=$rc"; if [ $rc -ge 124 ]; then echo "FAULT/TIMEOUT in $name: stopping"; exit $rc; fi; }
 STEPS=${STEPS:-all}
 if [[ $STEPS == all || $STEPS == *tests* ]]; then
-  timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1; stop_on_fault $? pytest
+  timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; stop_on_fault $? pytest
   tail -5 gpurun_out/pytest_gpu.log
 fi
 if [[ $STEPS == all || $STEPS == *smoke* ]]; then
