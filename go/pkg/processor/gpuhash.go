@@ -1,0 +1,253 @@
+// GPU-batched SHA-256 for MirBFT's hash path, backed by libmirsha (the C ABI in
+// include/mirsha.h of the mirbft_amd repository).
+//
+// This file belongs in the reference tree at pkg/processor/gpuhash.go (package
+// processor); go/wiring.patch adds the three call sites that use it. It replaces,
+// for a whole batch at a time:
+//
+//   - ProcessHashActions (pkg/processor/serial.go:180-198): ProcessHashActionsGPU
+//     has the same arguments, the same result order, the same Origin pointers and
+//     the same error for a non-hash action, but makes ONE libmirsha call per
+//     ActionList instead of one hash.Hash per action;
+//   - the request digest of Client.Propose (pkg/processor/clients.go:189-192):
+//     Client.ProposeBatch hashes several requests in one call, then runs
+//     Propose's own bookkeeping (proposeDigest, split out of Propose by the
+//     patch) for each request in order.
+//
+// The per-message processor.Hasher (crypto.SHA256) stays what the node uses for
+// single Propose calls and the testengine's application hash chain; libmirsha
+// has no CPU fallback of its own.
+//
+// cgo rules followed here: Go memory passed to C holds no Go pointers (the
+// [][]byte parts are packed into one arena first), and the arena and digest
+// buffers are page-locked C memory from msha_pinned_alloc, so the library DMAs
+// them as is. Digests are copied into fresh Go slices: the state machine keeps
+// them as map keys (batch_tracker.go:85-91, epoch_change.go:42-50).
+//
+// Go 1.15 compatible (go.mod:3): no generics, no unsafe.Slice.
+package processor
+
+/*
+#cgo CFLAGS: -I${SRCDIR}/../../third_party/mirsha/include
+#cgo LDFLAGS: -L${SRCDIR}/../../third_party/mirsha/lib -lmirsha -Wl,-rpath,${SRCDIR}/../../third_party/mirsha/lib
+#include <stdlib.h>
+#include "mirsha.h"
+*/
+import "C"
+
+import (
+	"sync"
+	"unsafe"
+
+	"github.com/pkg/errors"
+
+	"github.com/hyperledger-labs/mirbft/pkg/pb/state"
+	"github.com/hyperledger-labs/mirbft/pkg/statemachine"
+)
+
+// GPUHasher owns one libmirsha context (on the GPUs of its device mask) and two
+// pinned buffers: the packing arena and the digest output. A context serves one
+// thread at a time (mirsha.h); the mutex lets the hash goroutine (mirbft.go:470)
+// and ProposeBatch callers share one GPUHasher.
+type GPUHasher struct {
+	mutex  sync.Mutex
+	ctx    *C.msha_ctx
+	arena  pinnedBuf
+	out    pinnedBuf
+	off    []uint64
+	length []uint64
+}
+
+type pinnedBuf struct {
+	base unsafe.Pointer
+	buf  []byte
+}
+
+// NewGPUHasher creates a libmirsha context over the GPUs in deviceMask (bit i
+// = HIP device i; 0 means device 0). Independent hash actions are sharded over
+// them by cumulative block count; there is no collective.
+func NewGPUHasher(deviceMask uint32) (*GPUHasher, error) {
+	var ctx *C.msha_ctx
+	var errbuf [512]C.char
+	// The creation error travels with the call (msha_ctx_create_err): a
+	// goroutine may resume on another OS thread between two cgo calls.
+	rc := C.msha_ctx_create_err(C.uint32_t(deviceMask), &ctx, &errbuf[0], C.uint64_t(len(errbuf)))
+	if rc != C.MSHA_OK {
+		return nil, errors.Errorf("libmirsha error %d: %s", int(rc), C.GoString(&errbuf[0]))
+	}
+	return &GPUHasher{ctx: ctx}, nil
+}
+
+// Close releases the pinned buffers and the context.
+func (g *GPUHasher) Close() {
+	g.mutex.Lock()
+	defer g.mutex.Unlock()
+	if g.ctx == nil {
+		return
+	}
+	for _, p := range []*pinnedBuf{&g.arena, &g.out} {
+		if p.base != nil {
+			C.msha_pinned_free(g.ctx, p.base)
+			p.base, p.buf = nil, nil
+		}
+	}
+	C.msha_ctx_destroy(g.ctx)
+	g.ctx = nil
+}
+
+func (g *GPUHasher) fail(rc C.int) error {
+	// msha_last_error(ctx) is per context, and the context is used under g.mutex
+	// only, so the text belongs to this call whatever thread reads it.
+	return errors.Errorf("libmirsha error %d: %s", int(rc), C.GoString(C.msha_last_error(g.ctx)))
+}
+
+// ensure returns p's buffer resized to n bytes (grown in pinned memory on demand).
+func (g *GPUHasher) ensure(p *pinnedBuf, n int) ([]byte, error) {
+	if cap(p.buf) >= n {
+		p.buf = p.buf[:n]
+		return p.buf, nil
+	}
+	if p.base != nil {
+		C.msha_pinned_free(g.ctx, p.base)
+		p.base, p.buf = nil, nil
+	}
+	size := n + n/4 + 4096
+	var ptr unsafe.Pointer
+	if rc := C.msha_pinned_alloc(g.ctx, C.uint64_t(size), &ptr); rc != C.MSHA_OK {
+		return nil, g.fail(rc)
+	}
+	p.base = ptr
+	p.buf = (*[1 << 40]byte)(ptr)[:n:size]
+	return p.buf, nil
+}
+
+// digests hashes n messages in one msha_digest_batch call. size bounds the
+// packed arena (every message's bytes plus up to 15 bytes of alignment); pack(i,
+// dst) copies message i's bytes to dst and returns their count. Messages are
+// placed 16-byte aligned, so the library uploads the arena without a staging
+// copy. Returns n fresh 32-byte digests.
+func (g *GPUHasher) digests(n int, size int, pack func(i int, dst []byte) int) ([][]byte, error) {
+	g.mutex.Lock()
+	defer g.mutex.Unlock()
+	if g.ctx == nil {
+		return nil, errors.New("libmirsha: GPUHasher is closed")
+	}
+	result := make([][]byte, n)
+	if n == 0 {
+		return result, nil
+	}
+	arena, err := g.ensure(&g.arena, size+64)
+	if err != nil {
+		return nil, err
+	}
+	out, err := g.ensure(&g.out, 32*n)
+	if err != nil {
+		return nil, err
+	}
+	if cap(g.off) < n {
+		g.off = make([]uint64, n)
+		g.length = make([]uint64, n)
+	}
+	off, length := g.off[:n], g.length[:n]
+	pos := 0
+	for i := 0; i < n; i++ {
+		off[i] = uint64(pos)
+		l := pack(i, arena[pos:])
+		length[i] = uint64(l)
+		pos = (pos + l + 15) &^ 15
+	}
+	rc := C.msha_digest_batch(g.ctx,
+		(*C.uint8_t)(unsafe.Pointer(&arena[0])), C.uint64_t(pos),
+		(*C.uint64_t)(unsafe.Pointer(&off[0])), (*C.uint64_t)(unsafe.Pointer(&length[0])),
+		C.uint64_t(n), (*C.uint8_t)(unsafe.Pointer(&out[0])))
+	if rc != C.MSHA_OK {
+		return nil, g.fail(rc)
+	}
+	digests := make([]byte, 32*n) // one allocation; each digest a capacity-capped slice of it
+	copy(digests, out)
+	for i := range result {
+		result[i] = digests[32*i : 32*i+32 : 32*i+32]
+	}
+	return result, nil
+}
+
+// ProcessHashActionsGPU is a drop-in for ProcessHashActions (serial.go:180-198):
+// one HashResult per action, in input order, Digest = SHA-256 of the action's
+// Data parts concatenated (h.Write appends; zero parts hash the empty string),
+// Origin the same pointer as the action's; a non-hash action fails the whole
+// list with the reference's error text. One libmirsha call per ActionList.
+func ProcessHashActionsGPU(g *GPUHasher, actions *statemachine.ActionList) (*statemachine.EventList, error) {
+	reqs := make([]*state.ActionHashRequest, 0, actions.Len())
+	size := 0
+	iter := actions.Iterator()
+	for action := iter.Next(); action != nil; action = iter.Next() {
+		switch t := action.Type.(type) {
+		case *state.Action_Hash:
+			reqs = append(reqs, t.Hash)
+			for _, data := range t.Hash.Data {
+				size += len(data)
+			}
+			size += 15
+		default:
+			return nil, errors.Errorf("unexpected type for Hash action: %T", action.Type)
+		}
+	}
+
+	digests, err := g.digests(len(reqs), size, func(i int, dst []byte) int {
+		n := 0
+		for _, data := range reqs[i].Data {
+			n += copy(dst[n:], data)
+		}
+		return n
+	})
+	if err != nil {
+		return nil, err
+	}
+
+	events := &statemachine.EventList{}
+	for i, r := range reqs {
+		events.HashResult(digests[i], r.Origin)
+	}
+	return events, nil
+}
+
+// ProposedRequest is one request of a ProposeBatch call.
+type ProposedRequest struct {
+	ReqNo uint64
+	Data  []byte
+}
+
+// RequestDigests returns SHA-256(data) for every request (clients.go:190-192),
+// computed in one libmirsha call.
+func (g *GPUHasher) RequestDigests(reqs []ProposedRequest) ([][]byte, error) {
+	size := 0
+	for _, r := range reqs {
+		size += len(r.Data) + 15
+	}
+	return g.digests(len(reqs), size, func(i int, dst []byte) int {
+		return copy(dst, reqs[i].Data)
+	})
+}
+
+// ProposeBatch is Client.Propose (clients.go:189-276) for several requests of
+// this client. Their digests come from one libmirsha call; then each request
+// runs Propose's bookkeeping (proposeDigest) in order, so the request store,
+// the allocation state and the returned events are exactly those of calling
+// Propose once per request in the same order. The result is the concatenation
+// of the per-request event lists; the first error stops the batch and is
+// returned with the events of the requests before it.
+func (c *Client) ProposeBatch(g *GPUHasher, reqs []ProposedRequest) (*statemachine.EventList, error) {
+	digests, err := g.RequestDigests(reqs)
+	if err != nil {
+		return nil, errors.WithMessage(err, "could not hash requests")
+	}
+	events := &statemachine.EventList{}
+	for i, r := range reqs {
+		el, err := c.proposeDigest(r.ReqNo, r.Data, digests[i])
+		if err != nil {
+			return events, err
+		}
+		events.PushBackList(el)
+	}
+	return events, nil
+}
