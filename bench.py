@@ -306,6 +306,19 @@ def time_steps(step, args, dev, stream, barrier=None):
     return elapsed, kern_ms, warm, warmup_ms
 
 
+def algorithmic_bytes(w, cfg: str) -> int:
+    """HBM bytes one launch must move: payload read + metadata read + digests written.
+    Arena forms: payload + off/len (16 B) + order (4 B, mixed sizes) + 32 B out per
+    message; digest-of-digests (c3dd): 32 B per part digest + its 4-B index, 8 B per
+    begin entry, 32 B out per Batch."""
+    if cfg == "c3dd":
+        parts = int(w.idx.size)
+        return 32 * parts + 4 * parts + 8 * (w.n + 1) + 32 * w.n
+    order = 0 if w.uniform_stride else 4 * w.n
+    meta = 0 if cfg.startswith("u:") else 16 * w.n + order
+    return w.message_bytes + meta + 32 * w.n
+
+
 def roofline(w, kern_ms: float, cfg: str) -> dict:
     achieved = OPS_PER_BLOCK * w.blocks / (kern_ms * 1e-3) / 1e12
     traffic, src = measured_traffic(cfg)
@@ -316,7 +329,7 @@ def roofline(w, kern_ms: float, cfg: str) -> dict:
                     "instr at 2.4 GHz); SHA-256's mix is ~60% half-rate ops (v_alignbit, "
                     "v_add3) and costs ~3.9-4.1 SIMD cycles per instruction on gfx950 "
                     "(DESIGN.md, profiles/r01_valu_microbench*, r01_pmc.json)",
-            "algorithmic_bytes_per_launch": w.message_bytes + 32 * w.n + 16 * w.n,
+            "algorithmic_bytes_per_launch": algorithmic_bytes(w, cfg),
             "bare_loop_reference": BARE_LOOP_TOPS,
             "frac_of_bare_loop": achieved / BARE_LOOP_TOPS}
 
@@ -405,7 +418,17 @@ def main():
     if world > 1:
         # Control plane only (rendezvous, barrier, max-over-ranks): the hash path
         # has no data exchange between GPUs, so no RCCL communicator is created.
-        dist.init_process_group("gloo")
+        # Gloo prints its connection handshake on stdout; keep stdout to rank 0's
+        # one JSON line.
+        sys.stdout.flush()
+        saved, devnull = os.dup(1), os.open(os.devnull, os.O_WRONLY)
+        os.dup2(devnull, 1)
+        try:
+            dist.init_process_group("gloo")
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
+            os.close(devnull)
     if args.share_device:
         local = 0
     torch.cuda.set_device(local)

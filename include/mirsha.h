@@ -221,6 +221,11 @@ uint64_t msha_blocks_for_len(uint64_t len);
 int msha_order_by_blocks(const uint64_t* len, uint64_t n, uint32_t* order);
 int msha_partition_by_blocks(const uint64_t* len, uint64_t n, uint32_t n_shards,
                              uint64_t* bounds);
+/* Alias detection the host entry points run before hashing (EpochChange
+ * payloads re-hashed N^2 times, epoch_target.go:486-505): first[i] = the
+ * smallest j <= i with (off[j], len[j]) == (off[i], len[i]); such messages are
+ * hashed once and share the digest. */
+int msha_alias_first(const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* first);
 
 #ifdef __cplusplus
 }

@@ -105,6 +105,7 @@ SIGNATURES = {
     "msha_blocks_for_len": (ctypes.c_uint64, [ctypes.c_uint64]),
     "msha_order_by_blocks": (ctypes.c_int, [_u64p, ctypes.c_uint64, _u32p]),
     "msha_partition_by_blocks": (ctypes.c_int, [_u64p, ctypes.c_uint64, ctypes.c_uint32, _u64p]),
+    "msha_alias_first": (ctypes.c_int, [_u64p, _u64p, ctypes.c_uint64, _u64p]),
 }
 
 _lib = None

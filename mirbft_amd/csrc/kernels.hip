@@ -393,15 +393,18 @@ struct ArenaSrc {  // messages arena[off[m] : off[m]+len[m]] (k_digest_batch's f
 
 // Batch / VerifyBatch digests over a table of 32-byte digests
 // (k_digest_of_digests' form): block b < cnt/2 holds digests 2b and 2b+1.
-__device__ __forceinline__ void dod_pair_block(const uint4* tab, const uint32_t* idx, uint64_t k,
-                                               uint32_t (&w)[16]) {
-  const uint4* d0 = tab + 2 * (uint64_t)idx[k];
-  const uint4* d1 = tab + 2 * (uint64_t)idx[k + 1];
+__device__ __forceinline__ void dod_pair_words(const uint4* tab, uint32_t i0, uint32_t i1, uint32_t (&w)[16]) {
+  const uint4* d0 = tab + 2 * (uint64_t)i0;
+  const uint4* d1 = tab + 2 * (uint64_t)i1;
   uint4 v0 = d0[0], v1 = d0[1], v2 = d1[0], v3 = d1[1];
   w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
   w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
   w[8] = bswap(v2.x); w[9] = bswap(v2.y); w[10] = bswap(v2.z); w[11] = bswap(v2.w);
   w[12] = bswap(v3.x); w[13] = bswap(v3.y); w[14] = bswap(v3.z); w[15] = bswap(v3.w);
+}
+__device__ __forceinline__ void dod_pair_block(const uint4* tab, const uint32_t* idx, uint64_t k,
+                                               uint32_t (&w)[16]) {
+  dod_pair_words(tab, idx[k], idx[k + 1], w);
 }
 // The final block: the odd digest left (k < cnt), 0x80, zeros, the bit length.
 __device__ __forceinline__ void dod_final_block(const uint4* tab, const uint32_t* idx, uint64_t k,

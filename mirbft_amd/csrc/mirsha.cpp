@@ -392,51 +392,117 @@ struct Plan {
   bool identity() const { return !ordered && rep.empty(); }  // lane q hashes message q
 };
 
-// Direct mode with chunked uploads: when the lanes' payloads ascend through the
-// span (the common request batch: equal block counts, identity lane order, an
-// ascending arena), cut the lanes into groups by the span chunk that completes
-// their payload, so lane group g is hashed as soon as chunk cut_chunk[g] lands
-// and, for identity lanes, its digests come back while later chunks upload.
-void group_lanes_by_span_chunk(Plan& P, const uint64_t* h_off, const uint64_t* h_len,
-                               uint64_t span) {
-  const uint64_t chunks = std::max<uint64_t>(1, (span + kDirectChunk - 1) / kDirectChunk);
-  const uint64_t n = P.lanes;
-  auto chunk_of = [&](uint64_t q) {
-    const uint64_t end = h_off[q] + std::max<uint64_t>(h_len[q], 1) - 1;
-    return std::min<uint64_t>(end / kDirectChunk, chunks - 1);
-  };
-  if (chunks == 1 || n == 0) {
-    P.cut_chunk.assign(1, chunks - 1);
-    return;
-  }
-  const unsigned T = plan_threads(n);
-  std::vector<uint8_t> mono(T, 1);
-  parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
-    for (uint64_t q = std::max<uint64_t>(a, 1); q < b; ++q)
-      if (chunk_of(q) < chunk_of(q - 1)) { mono[t] = 0; break; }
+
+// Direct mode: order the shard's lanes (one per distinct payload: rep[i] == i,
+// or every message when rep is empty) and fill their lane-indexed device
+// offsets and lengths, in one fused counting sort. Key = (device upload chunk
+// holding the END of the payload, descending block count): lanes are grouped by
+// the 64 MiB chunk (kDirectChunk) whose event says their payload has landed,
+// so each group is hashed as soon as it lands (c5: the ~13 ms kernel runs
+// under the upload instead of after it), and inside a group a wave's lanes
+// have equal block counts. Stable (index order inside a bucket). Two
+// sequential passes over the messages and one scatter; a request batch whose
+// keys already ascend with the index (identity lanes) skips the scatter.
+// Sets perm, lanes (unchanged), ordered, lane_cut and cut_chunk; h_off/h_len
+// are lane-indexed; tdev is scratch (device offset per message).
+void plan_direct_lanes(Plan& P, const Device& d, const uint64_t* off, const uint64_t* len,
+                       uint64_t* h_off, uint64_t* h_len, std::vector<uint64_t>& tdev) {
+  const uint64_t m = P.m;
+  const bool all = P.rep.empty();
+  const uint32_t* rep = P.rep.data();
+  auto lane = [&](uint64_t i) { return all || rep[i] == i; };
+  const uint64_t chunks = std::max<uint64_t>(1, (d.arena_bytes + kDirectChunk - 1) / kDirectChunk);
+  const unsigned T = plan_threads(m);
+  tdev.resize(m);
+  // pass 0: device offsets, the largest block count
+  std::vector<uint64_t> tmax(T, 0);
+  parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t mx = 0;
+    for (uint64_t i = a; i < b; ++i) {
+      tdev[i] = d.direct_remap(off[i]);
+      if (lane(i)) mx = std::max(mx, blocks_for(len[i]));
+    }
+    tmax[t] = mx;
   });
-  if (std::find(mono.begin(), mono.end(), 0) != mono.end()) {
-    // Lanes ordered by block count run all over the span: one group, after the
-    // last chunk. (Regrouping them costs a sort of every lane on the host,
-    // ~40 ms for 8 M lanes, for a few ms of kernel overlap.)
-    P.cut_chunk.assign(1, chunks - 1);
-    return;
+  uint64_t bmax = *std::max_element(tmax.begin(), tmax.end());
+  // bucket = chunk * B + (bmax - blocks); block classes only while the
+  // per-thread histograms stay small (then: by chunk alone)
+  const bool by_blocks = chunks * (bmax + 1) <= (1u << 20);
+  const uint64_t B = by_blocks ? bmax + 1 : 1;
+  const uint64_t nb = chunks * B;
+  auto key = [&](uint64_t i) -> uint64_t {
+    const uint64_t c = std::min<uint64_t>((tdev[i] + std::max<uint64_t>(len[i], 1) - 1) / kDirectChunk, chunks - 1);
+    return c * B + (by_blocks ? bmax - blocks_for(len[i]) : 0);
+  };
+  // pass 1: histograms; are the keys already ascending (identity order)?
+  std::vector<uint64_t> cnt((size_t)T * nb, 0);
+  std::vector<uint64_t> first_key(T, UINT64_MAX), last_key(T, 0);
+  std::vector<uint8_t> mono(T, 1);
+  parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t* c = cnt.data() + (size_t)t * nb;
+    uint64_t prev = 0;
+    bool first = true, asc = true;
+    for (uint64_t i = a; i < b; ++i) {
+      if (!lane(i)) continue;
+      const uint64_t k = key(i);
+      c[k]++;
+      if (first) {
+        first_key[t] = k;
+        first = false;
+      } else if (k < prev) {
+        asc = false;
+      }
+      prev = k;
+    }
+    last_key[t] = prev;
+    mono[t] = asc;
+  });
+  bool identity = all;
+  for (unsigned t = 0; t < T && identity; ++t) identity = mono[t];
+  for (unsigned t = 1; t < T && identity; ++t)
+    if (first_key[t] != UINT64_MAX && first_key[t] < last_key[t - 1]) identity = false;
+  // group starts by chunk: lanes with bucket < c * B come before chunk c
+  std::vector<uint64_t> chunk_lanes(chunks, 0);
+  for (unsigned t = 0; t < T; ++t)
+    for (uint64_t k = 0; k < nb; ++k) chunk_lanes[k / B] += cnt[(size_t)t * nb + k];
+  if (identity) {
+    parallel_chunks(m, T, [&](unsigned, uint64_t a, uint64_t b) {
+      for (uint64_t i = a; i < b; ++i) {
+        P.perm[i] = (uint32_t)i;
+        h_off[i] = tdev[i];
+        h_len[i] = len[i];
+      }
+    });
+    P.ordered = false;
+  } else {
+    uint64_t run = 0;  // bucket-major, then thread (= index) order: stable
+    for (uint64_t k = 0; k < nb; ++k)
+      for (unsigned t = 0; t < T; ++t) {
+        const uint64_t x = cnt[(size_t)t * nb + k];
+        cnt[(size_t)t * nb + k] = run;
+        run += x;
+      }
+    parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
+      uint64_t* c = cnt.data() + (size_t)t * nb;
+      for (uint64_t i = a; i < b; ++i) {
+        if (!lane(i)) continue;
+        const uint64_t q = c[key(i)]++;
+        P.perm[q] = (uint32_t)i;
+        h_off[q] = tdev[i];
+        h_len[q] = len[i];
+      }
+    });
+    P.ordered = true;
   }
-  // one lane group per chunk that completes at least one payload (binary
-  // searches over the monotone chunk index)
+  // lane groups: one per chunk that completes at least one payload
   P.lane_cut.assign(1, 0);
   P.cut_chunk.clear();
-  for (uint64_t q = 0; q < n;) {
-    const uint64_t c = chunk_of(q);
-    uint64_t lo = q + 1, hi = n;  // first lane past chunk c
-    while (lo < hi) {
-      const uint64_t mid = lo + (hi - lo) / 2;
-      if (chunk_of(mid) <= c) lo = mid + 1;
-      else hi = mid;
-    }
-    P.lane_cut.push_back(lo);
+  uint64_t acc = 0;
+  for (uint64_t c = 0; c < chunks; ++c) {
+    if (!chunk_lanes[c]) continue;
+    acc += chunk_lanes[c];
+    P.lane_cut.push_back(acc);
     P.cut_chunk.push_back(c);
-    q = lo;
   }
 }
 
@@ -448,7 +514,7 @@ struct msha_ctx {
   msha_stats stats{};
   std::vector<void*> pinned;  // allocations handed out by msha_pinned_alloc
   std::vector<uint32_t> sort_tmp;
-  std::vector<uint64_t> tmp_len;
+  std::vector<uint64_t> tmp_len, tmp_dev;
   int kernel_policy = MSHA_KERNEL_AUTO;
   // host planning buffers reused across calls
   std::vector<Plan> plans;
@@ -533,43 +599,124 @@ bool is_pinned_host(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
+inline uint32_t alias_tag(uint64_t off, uint64_t len) {
+  uint64_t h = off ^ (len * 0x9E3779B97F4A7C15ull);  // splitmix64 finalizer over both fields
+  h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
+  h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
+  return (uint32_t)((h ^ (h >> 31)) >> 32);
+}
+
 // uid[i] = the first index j <= i with (off[j], len[j]) == (off[i], len[i]).
-// Open addressing (linear probing) over R regions picked by the key hash's top
-// bits. Pass 1 hashes every key and counts keys per (index chunk, region);
-// pass 2 scatters (tag << 32 | index) into per-region buckets, in index order;
-// pass 3 builds each region's table on its own worker from its bucket alone,
-// prefetching the slot of the key kPrefetch ahead (the probes are the cost:
-// random accesses into a table far larger than the caches). A table entry is
-// (tag << 32) | (index + 1); off/len are dereferenced only on a tag match, and
-// "first" is preserved because a region inserts its keys in index order.
+//
+// Candidates first: a message whose offset is greater than every earlier
+// message's ("forward") cannot repeat an earlier payload, so uid[i] = i. Only
+// the others (offset at or below an earlier one) can be aliases. A batch of
+// requests and batches packed in order plus a shared pool of EpochChange
+// payloads (c5: ~5 % of the actions point back into the pool) has few of them,
+// so the table is built over the candidates only and the forward messages just
+// probe it (each key has at most one forward message: its offset is unique),
+// instead of inserting all n keys (c5, 8 M actions: 22 ms -> a few ms).
+// With more than n/4 candidates the table simply takes every message.
+//
+// The table: open addressing (linear probing) over R regions picked by the key
+// hash's top bits. Pass 1 hashes every key and counts keys per (index chunk,
+// region); pass 2 scatters (tag << 32 | index) into per-region buckets, in
+// index order; pass 3 builds each region's table on its own worker from its
+// bucket alone, prefetching the slot of the key kPrefetch ahead (the probes are
+// the cost: random accesses into a table far larger than the caches). A table
+// entry is (tag << 32) | (index + 1); off/len are dereferenced only on a tag
+// match, and "first" is preserved because a region inserts its keys in index order.
 void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vector<uint64_t>& uid,
                 std::vector<uint64_t>& table, std::vector<uint64_t>& bucket, std::vector<uint32_t>& tagv) {
   uid.resize(n);
-  bucket.resize(n);
   tagv.resize(n);
-  const unsigned rbits = n >= (1u << 20) ? 4 : 0;
-  const unsigned R = 1u << rbits;  // regions (one pass-3 task each)
   const unsigned T = plan_threads(n);
-  std::vector<uint64_t> cnt((size_t)T * R, 0);
-  // pass 1: one hash per key (splitmix64 finalizer over both fields) -> its 32-bit tag
+  // forward messages (uid = self) and the candidate list, in index order
+  std::vector<uint64_t> cmax(T, 0);
   parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
-    uint64_t* c = cnt.data() + (size_t)t * R;
+    uint64_t mx = 0;
+    for (uint64_t i = a; i < b; ++i) mx = std::max(mx, off[i] + 1);
+    cmax[t] = mx;
+  });
+  // the forward pass also hashes every key (the probe below reads the tags)
+  // and copies each candidate's key out while it streams off/len
+  struct Cand {
+    std::vector<uint32_t> idx;
+    std::vector<uint64_t> off, len;
+  };
+  std::vector<Cand> tcand(T);
+  parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t run = 0;  // max(off + 1) over every earlier message
+    for (unsigned u = 0; u < t; ++u) run = std::max(run, cmax[u]);
+    Cand& c = tcand[t];
     for (uint64_t i = a; i < b; ++i) {
-      uint64_t h = off[i] ^ (len[i] * 0x9E3779B97F4A7C15ull);
-      h = (h ^ (h >> 30)) * 0xBF58476D1CE4E5B9ull;
-      h = (h ^ (h >> 27)) * 0x94D049BB133111EBull;
-      const uint32_t tag = (uint32_t)((h ^ (h >> 31)) >> 32);
-      tagv[i] = tag;
+      tagv[i] = alias_tag(off[i], len[i]);
+      if (off[i] + 1 > run) {
+        uid[i] = i;
+        run = off[i] + 1;
+      } else {
+        uid[i] = UINT64_MAX;  // candidate: resolved below
+        c.idx.push_back((uint32_t)i);
+        c.off.push_back(off[i]);
+        c.len.push_back(len[i]);
+      }
+    }
+  });
+  uint64_t m = 0;
+  for (auto& c : tcand) m += c.idx.size();
+  if (m == 0) return;
+  const bool subset = m <= n / 4;
+  // Items of the table: the candidates (subset mode; their keys in compact
+  // arrays, so the table build does not miss the cache on every key) or every
+  // message. Item k's key is (ko[k], kl[k]); its message is cand[k] (or k).
+  std::vector<uint32_t> cand;
+  std::vector<uint64_t> cko, ckl;
+  if (subset) {
+    cand.resize(m);
+    cko.resize(m);
+    ckl.resize(m);
+    std::vector<uint64_t> at(T + 1, 0);
+    for (unsigned t = 0; t < T; ++t) at[t + 1] = at[t] + tcand[t].idx.size();
+    const std::function<void(unsigned)> copy = [&](unsigned t) {
+      const Cand& c = tcand[t];
+      std::memcpy(cand.data() + at[t], c.idx.data(), 4 * c.idx.size());
+      std::memcpy(cko.data() + at[t], c.off.data(), 8 * c.off.size());
+      std::memcpy(ckl.data() + at[t], c.len.data(), 8 * c.len.size());
+    };
+    if (T == 1) copy(0);
+    else WorkerPool::get().run(T, copy);
+  } else {
+    m = n;
+  }
+  tcand.clear();
+  const uint64_t* ko = subset ? cko.data() : off;
+  const uint64_t* kl = subset ? ckl.data() : len;
+  bucket.resize(m);
+  const unsigned rbits = m >= (1u << 20) ? 4 : 0;
+  const unsigned R = 1u << rbits;  // regions (one pass-3 task each)
+  const unsigned Tm = plan_threads(m);
+  std::vector<uint64_t> cnt((size_t)Tm * R, 0);
+  // item k's tag, then (subset mode) the table slot of its key; every
+  // message's tag stays in tagv for the forward probe
+  std::vector<uint32_t> ctag;
+  std::vector<uint32_t>& tag_k = subset ? ctag : tagv;
+  if (subset) ctag.resize(m);
+  // pass 1: region histogram (subset mode: the candidates' tags, from their keys)
+  parallel_chunks(m, Tm, [&](unsigned t, uint64_t a, uint64_t b) {
+    uint64_t* c = cnt.data() + (size_t)t * R;
+    for (uint64_t k = a; k < b; ++k) {
+      const uint32_t tag = subset ? alias_tag(ko[k], kl[k]) : tagv[k];
+      tag_k[k] = tag;
       ++c[rbits ? tag >> (32 - rbits) : 0];
     }
   });
   // bucket layout: region-major, chunk order inside a region (= index order)
-  std::vector<uint64_t> rstart(R + 1, 0), base((size_t)T * R);
+  std::vector<uint64_t> rstart(R + 1, 0), base((size_t)Tm * R);
   {
     uint64_t acc = 0;
     for (unsigned r = 0; r < R; ++r) {
       rstart[r] = acc;
-      for (unsigned t = 0; t < T; ++t) {
+      for (unsigned t = 0; t < Tm; ++t) {
         base[(size_t)t * R + r] = acc;
         acc += cnt[(size_t)t * R + r];
       }
@@ -577,11 +724,11 @@ void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vecto
     rstart[R] = acc;
   }
   // pass 2: scatter
-  parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
+  parallel_chunks(m, Tm, [&](unsigned t, uint64_t a, uint64_t b) {
     uint64_t* w = base.data() + (size_t)t * R;
-    for (uint64_t i = a; i < b; ++i) {
-      const uint32_t tag = tagv[i];
-      bucket[w[rbits ? tag >> (32 - rbits) : 0]++] = (uint64_t)tag << 32 | i;
+    for (uint64_t k = a; k < b; ++k) {
+      const uint32_t tag = tag_k[k];
+      bucket[w[rbits ? tag >> (32 - rbits) : 0]++] = (uint64_t)tag << 32 | k;
     }
   });
   // per-region table capacity: a power of two >= 2x its keys
@@ -593,36 +740,80 @@ void alias_uids(const uint64_t* off, const uint64_t* len, uint64_t n, std::vecto
     tstart[r + 1] = tstart[r] + c;
   }
   if (table.size() < tstart[R]) table.resize(tstart[R]);
-  // pass 3: one task per region
-  static const uint64_t kPrefetch = getenv("PF") ? atoi(getenv("PF")) : 16;
+  // pass 3: one task per region. first_k[k] = the first item with k's key;
+  // in subset mode tag_k[k] becomes the global slot of k's key (for the
+  // forward probe below).
+  std::vector<uint32_t> first_k(subset ? m : 0);
+  constexpr uint64_t kPrefetch = 16;
   const std::function<void(unsigned)> build = [&](unsigned r) {
     uint64_t* reg = table.data() + tstart[r];
     const uint64_t mask = cap[r] - 1;
     std::memset(reg, 0, cap[r] * sizeof(uint64_t));  // 0 = empty
     const uint64_t* bk = bucket.data() + rstart[r];
-    const uint64_t m = rstart[r + 1] - rstart[r];
-    for (uint64_t k = 0; k < m; ++k) {
-      const uint64_t ahead = k + kPrefetch < m ? bk[k + kPrefetch] : bk[k];
+    const uint64_t cnt_r = rstart[r + 1] - rstart[r];
+    for (uint64_t q = 0; q < cnt_r; ++q) {
+      const uint64_t ahead = q + kPrefetch < cnt_r ? bk[q + kPrefetch] : bk[q];
       __builtin_prefetch(reg + ((ahead >> 32) & mask), 1);
-      const uint64_t e0 = bk[k];
-      const uint64_t i = e0 & 0xffffffffull, tag = e0 & 0xffffffff00000000ull;
+      const uint64_t e0 = bk[q];
+      const uint64_t k = e0 & 0xffffffffull, tag = e0 & 0xffffffff00000000ull;
       for (uint64_t p = (e0 >> 32) & mask;; p = (p + 1) & mask) {
         const uint64_t e = reg[p];
+        uint64_t j = k;
         if (e == 0) {
-          reg[p] = tag | (i + 1);
-          uid[i] = i;
-          break;
+          reg[p] = tag | (k + 1);
+        } else {
+          j = (e & 0xffffffffull) - 1;
+          if ((e & 0xffffffff00000000ull) != tag || ko[j] != ko[k] || kl[j] != kl[k]) continue;
         }
-        const uint64_t j = (e & 0xffffffffull) - 1;
-        if ((e & 0xffffffff00000000ull) == tag && off[j] == off[i] && len[j] == len[i]) {
-          uid[i] = j;
-          break;
+        if (subset) {
+          first_k[k] = (uint32_t)j;
+          tag_k[k] = (uint32_t)(tstart[r] + p);
+        } else {
+          uid[k] = j;
         }
+        break;
       }
     }
   };
   if (R == 1) build(0);
   else WorkerPool::get().run(R, build);
+  if (!subset) return;
+  // Forward messages that carry a candidate's key are its first occurrence
+  // (an offset above every earlier one precedes every repeat of it). A 2^20-bit
+  // filter over the candidates' tags (128 KiB, cache-resident) turns away
+  // almost every forward message before it touches the table.
+  std::vector<uint64_t> filter(1u << 14, 0);
+  for (uint64_t g = 0; g < tstart[R]; ++g)
+    if (table[g]) {
+      const uint32_t tag = (uint32_t)(table[g] >> 32);
+      filter[(tag >> 6) & 0x3fff] |= 1ull << (tag & 63);
+    }
+  std::vector<uint64_t> fwd(tstart[R], UINT64_MAX);
+  parallel_chunks(n, T, [&](unsigned, uint64_t a, uint64_t b) {
+    for (uint64_t i = a; i < b; ++i) {
+      if (uid[i] != i) continue;  // candidates: resolved below
+      const uint32_t tag = tagv[i];
+      if (!((filter[(tag >> 6) & 0x3fff] >> (tag & 63)) & 1)) continue;
+      const unsigned r = rbits ? tag >> (32 - rbits) : 0;
+      const uint64_t* reg = table.data() + tstart[r];
+      const uint64_t mask = cap[r] - 1;
+      for (uint64_t p = tag & mask;; p = (p + 1) & mask) {
+        const uint64_t e = reg[p];
+        if (e == 0) break;
+        const uint64_t j = (e & 0xffffffffull) - 1;
+        if ((e >> 32) == tag && ko[j] == off[i] && kl[j] == len[i]) {
+          fwd[tstart[r] + p] = i;  // i is forward: the first occurrence of the key
+          break;
+        }
+      }
+    }
+  });
+  parallel_chunks(m, Tm, [&](unsigned, uint64_t a, uint64_t b) {
+    for (uint64_t k = a; k < b; ++k) {
+      const uint64_t f = fwd[tag_k[k]];
+      uid[cand[k]] = f != UINT64_MAX ? f : cand[first_k[k]];
+    }
+  });
 }
 
 // Host-memory execution of one batch (the body of every host entry point):
@@ -827,19 +1018,43 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       for (uint64_t c : nl) P.lanes += c;
       if (P.lanes == P.m) P.rep.clear();
     } else if (uid) {
+      // rep[i] = the shard-local index of the shard's first message with i's
+      // payload. uid[i] (the batch-wide first occurrence) at or past the shard's
+      // start lies in this shard, so it is also the shard's first: threaded.
+      // An earlier uid (a payload first seen by an earlier shard, e.g. the shared
+      // EpochChange pool) is resolved in index order through `placed`, over
+      // those messages only.
       P.rep.resize(P.m);
-      P.lanes = 0;
-      for (uint64_t i = 0; i < P.m; ++i) {
-        uint64_t& first = placed[uid[d.lo + i]];
-        if (first == UINT64_MAX) {
-          first = i;
-          touched.push_back(uid[d.lo + i]);
-          P.rep[i] = (uint32_t)i;
-          ++P.lanes;
-        } else {
-          P.rep[i] = (uint32_t)first;
+      const unsigned T = plan_threads(P.m);
+      std::vector<uint64_t> nl(T, 0);
+      std::vector<std::vector<uint32_t>> cross(T);
+      parallel_chunks(P.m, T, [&](unsigned t, uint64_t a, uint64_t b) {
+        uint64_t c = 0;
+        for (uint64_t i = a; i < b; ++i) {
+          const uint64_t u = uid[d.lo + i];
+          if (u >= d.lo) {
+            P.rep[i] = (uint32_t)(u - d.lo);
+            c += u == d.lo + i;
+          } else {
+            cross[t].push_back((uint32_t)i);
+          }
         }
-      }
+        nl[t] = c;
+      });
+      P.lanes = 0;
+      for (uint64_t c : nl) P.lanes += c;
+      for (const std::vector<uint32_t>& v : cross)
+        for (uint32_t i : v) {
+          uint64_t& first = placed[uid[d.lo + i]];
+          if (first == UINT64_MAX) {
+            first = i;
+            touched.push_back(uid[d.lo + i]);
+            P.rep[i] = i;
+            ++P.lanes;
+          } else {
+            P.rep[i] = (uint32_t)first;
+          }
+        }
       for (uint64_t t : touched) placed[t] = UINT64_MAX;
       touched.clear();
       if (P.lanes == P.m) P.rep.clear();
@@ -847,7 +1062,12 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     d.st.lanes = P.lanes;
     trace("representatives", t0);
     P.perm.resize(P.lanes);
-    if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
+    d.h_meta.ensure(16 * P.m + 4 * P.m);
+    uint64_t* h_off = d.h_meta.as<uint64_t>();
+    uint64_t* h_len = h_off + P.m;
+    if (direct) {
+      // direct mode orders the lanes and fills their metadata in one pass (below)
+    } else if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
       order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp, P.rep.data());
       P.ordered = true;
     } else {
@@ -856,25 +1076,13 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       else for (uint64_t i = 0; i < P.m; ++i) P.perm[i] = (uint32_t)i;
     }
     trace("lane order", t0);
-    d.h_meta.ensure(16 * P.m + 4 * P.m);
-    uint64_t* h_off = d.h_meta.as<uint64_t>();
-    uint64_t* h_len = h_off + P.m;
     // Place payloads in lane order (each lane's payload is distinct: aliases
     // were folded into their representative above), so every lane of chunk c
     // reads bytes uploaded by the end of chunk c.
     uint64_t acc = 0;
     if (direct) {  // the shard's byte ranges of the caller's pinned arena, uploaded as is
-      const unsigned T = plan_threads(P.lanes);
-      parallel_chunks(P.lanes, T, [&](unsigned, uint64_t a, uint64_t b) {
-        for (uint64_t q = a; q < b; ++q) {
-          const uint32_t i = P.perm[q];
-          h_off[q] = d.direct_remap(direct->off[d.lo + i]);
-          h_len[q] = L[i];
-        }
-      });
+      plan_direct_lanes(P, d, direct->off + d.lo, L, h_off, h_len, ctx->tmp_dev);
       acc = d.arena_bytes;
-      P.lane_cut.assign({0, P.lanes});
-      group_lanes_by_span_chunk(P, h_off, h_len, acc);
     } else {
       // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
       // (lane q's payload lands at h_off[q]; payloads are placed in lane order)
@@ -1231,6 +1439,20 @@ int msha_order_by_blocks(const uint64_t* len, uint64_t n, uint32_t* order) {
 int msha_partition_by_blocks(const uint64_t* len, uint64_t n, uint32_t n_shards, uint64_t* bounds) {
   if (!bounds || n_shards == 0 || (n && !len)) return MSHA_ERR_INVALID_ARG;
   partition(len, n, n_shards, bounds);
+  return MSHA_OK;
+}
+
+int msha_alias_first(const uint64_t* off, const uint64_t* len, uint64_t n, uint64_t* first) {
+  if (n && (!off || !len || !first)) return MSHA_ERR_INVALID_ARG;
+  if (n >= 0xffffffffull) return MSHA_ERR_INVALID_ARG;
+  try {
+    std::vector<uint64_t> uid, table, bucket;
+    std::vector<uint32_t> tag;
+    alias_uids(off, len, n, uid, table, bucket, tag);
+    std::memcpy(first, uid.data(), 8 * n);
+  } catch (...) {
+    return MSHA_ERR_OUT_OF_MEMORY;
+  }
   return MSHA_OK;
 }
 

@@ -53,6 +53,20 @@ def order_by_blocks(lengths: np.ndarray) -> np.ndarray:
     return order[: lengths.size]
 
 
+def alias_first(off: np.ndarray, length: np.ndarray) -> np.ndarray:
+    """first[i] = smallest j <= i with the same (off, len) (host-only helper)."""
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint64)
+    first = np.zeros(max(off.size, 1), dtype=np.uint64)
+    a = off if off.size else np.zeros(1, dtype=np.uint64)
+    b = length if length.size else np.zeros(1, dtype=np.uint64)
+    rc = L.lib().msha_alias_first(_p(a, ctypes.c_uint64), _p(b, ctypes.c_uint64), off.size,
+                                  _p(first, ctypes.c_uint64))
+    if rc != L.MSHA_OK:
+        raise MshaError(rc, "alias_first")
+    return first[: off.size]
+
+
 def device_count() -> int:
     n = ctypes.c_int(0)
     L.lib().msha_device_count(ctypes.byref(n))

@@ -149,3 +149,47 @@ def test_stats_and_shard_stats_null_args():
     assert lib.msha_get_shard_stats(None, 0, None) == L.MSHA_ERR_INVALID_ARG
     assert ctypes.sizeof(L.MshaShardStats) == 8 * 11
     assert ctypes.sizeof(L.MshaStats) == 8 * 17
+
+
+def _first_ref(off, ln):
+    seen, out = {}, np.empty(off.size, dtype=np.uint64)
+    for i, k in enumerate(zip(off.tolist(), ln.tolist())):
+        out[i] = seen.setdefault(k, i)
+    return out
+
+
+@pytest.mark.parametrize("case", ["forward", "pool", "all_alias", "zero_len", "random", "large_pool"])
+def test_alias_first_matches_dict(case):
+    """msha_alias_first (the host pipeline's alias detection, candidates-first):
+    forward-only batches, a shared pool pointed back into (c5 shape, both below
+    and above the 2^20-key region split), zero-length messages at shared
+    offsets, and dense random repeats (the whole-table path)."""
+    from mirbft_amd.engine import alias_first
+    rng = np.random.default_rng(len(case))
+    if case == "forward":
+        ln = rng.integers(0, 600, 50_000).astype(np.uint64)
+        off = np.concatenate([[0], np.cumsum((ln + 15) // 16 * 16)[:-1]]).astype(np.uint64)
+    elif case in ("pool", "large_pool"):
+        n = 60_000 if case == "pool" else (1 << 20) + 777
+        pool_off = np.arange(100, dtype=np.uint64) * np.uint64(4096)
+        pool_len = rng.integers(1, 4000, 100).astype(np.uint64)
+        kind = rng.random(n) < 0.05
+        pick = rng.integers(0, 100, n)
+        own_len = rng.integers(1, 640, n).astype(np.uint64)
+        own_off = np.uint64(1 << 20) + np.concatenate([[0], np.cumsum(own_len)[:-1]]).astype(np.uint64)
+        off = np.where(kind, pool_off[pick], own_off).astype(np.uint64)
+        ln = np.where(kind, pool_len[pick], own_len).astype(np.uint64)
+        if case == "pool":
+            off[7], ln[7] = off[3], ln[3]          # an own payload repeated later
+    elif case == "all_alias":
+        off = np.full(20_000, 64, dtype=np.uint64)
+        ln = np.full(20_000, 100, dtype=np.uint64)
+    elif case == "zero_len":
+        off = rng.integers(0, 50, 30_000).astype(np.uint64) * np.uint64(16)
+        ln = np.where(rng.random(30_000) < 0.5, 0, 16).astype(np.uint64)
+    else:
+        off = rng.integers(0, 5_000, 40_000).astype(np.uint64)
+        ln = rng.integers(0, 3, 40_000).astype(np.uint64)
+    got = alias_first(off, ln)
+    exp = _first_ref(off, ln)
+    assert np.array_equal(got, exp)

@@ -68,3 +68,23 @@ def test_partition_matches_rank_slicing_balance():
     per = np.array([blocks[b[i]:b[i + 1]].sum() for i in range(8)])
     assert per.sum() == blocks.sum()
     assert per.max() - per.min() <= blocks.max()
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_on_the_engine():
+    """bench.py --gpus 2 starts its own two rank processes (no torchrun
+    environment given) and each drives the HIP engine on its own disjoint c2
+    slice; on a one-GPU box both ranks share GPU 0 (--share-device). Rank 0's
+    stdout is exactly one JSON line with n_gpus 2 and the whole job's work."""
+    import json
+    import subprocess
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-device",
+                        "--steps", "5", "--warmup", "2", "--min-warmup-ms", "50", "--no-cpu-baseline"],
+                       env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["kernel"] == "lane"
+    assert d["value"] > 0 and d["config"]["messages_per_gpu"] == 1 << 20
