@@ -221,7 +221,11 @@ struct Device {
     return direct_map[r >> direct_gshift] + (r & ((1ull << direct_gshift) - 1));
   }
   msha_shard_stats st{};          // last host call (msha_get_shard_stats)
-  std::unique_ptr<WorkerPool> gather_pool;  // multi-GPU pageable calls: this GPU's gather helpers
+  // Multi-GPU host calls: this GPU's share of the host threads (its shard is
+  // planned, and its pageable chunks gathered, on them) and planning scratch.
+  std::unique_ptr<WorkerPool> gather_pool;
+  std::vector<uint32_t> sort_tmp;
+  std::vector<uint64_t> tmp_dev;
   // split chaining (kernels.hip): kSplitRing flag arrays of cus*2 entries,
   // allocated once and zeroed, never reallocated (launches may be in flight)
   uint64_t* split_flags = nullptr;
@@ -268,10 +272,14 @@ inline void trace(const char* what, double t0) {
 
 // Host planning of large batches runs on a few threads: [0, n) is split into
 // T contiguous chunks and f(t, lo, hi) runs for each (T = 1 below 256 K items).
+// The threads are those of the calling thread's pool: the process-wide one,
+// or, while one GPU's shard of a multi-GPU call is planned on a thread of its
+// own, that GPU's pool (tl_pool), so the shards are planned side by side.
+thread_local WorkerPool* tl_pool = nullptr;
+inline WorkerPool& cur_pool() { return tl_pool ? *tl_pool : WorkerPool::get(); }
 inline unsigned plan_threads(uint64_t n) {
   if (n < (1u << 18)) return 1;
-  const unsigned hw = std::thread::hardware_concurrency();
-  return std::max(1u, std::min(16u, hw));
+  return cur_pool().size();
 }
 template <class F>
 void parallel_chunks(uint64_t n, unsigned T, F&& f) {
@@ -280,7 +288,7 @@ void parallel_chunks(uint64_t n, unsigned T, F&& f) {
     return;
   }
   const std::function<void(unsigned)> job = [&](unsigned t) { f(t, n * t / T, n * (t + 1) / T); };
-  WorkerPool::get().run(T, job);
+  cur_pool().run(T, job);
 }
 
 // Descending-block-count permutation so every wavefront gets messages of equal
@@ -513,12 +521,11 @@ struct msha_ctx {
   std::string err;
   msha_stats stats{};
   std::vector<void*> pinned;  // allocations handed out by msha_pinned_alloc
-  std::vector<uint32_t> sort_tmp;
-  std::vector<uint64_t> tmp_len, tmp_dev;
+  std::vector<uint64_t> tmp_len;
   int kernel_policy = MSHA_KERNEL_AUTO;
   // host planning buffers reused across calls
   std::vector<Plan> plans;
-  std::vector<uint64_t> uid, placed;
+  std::vector<uint64_t> uid;
   std::vector<uint64_t> alias_table, alias_bucket;
   std::vector<uint32_t> alias_tag;
 };
@@ -574,6 +581,37 @@ void count_launch(msha_ctx* ctx, Device* d, msha::LaunchKind kind) {
   }
   __atomic_fetch_add(f, 1, __ATOMIC_RELAXED);
   if (d) d->st.launches++;
+}
+
+// Runs f(s) for every shard s of the context: inline for one shard; for
+// several, one thread per shard, each with its GPU's share of the host threads
+// as its planning pool (tl_pool), so per-GPU work (upload queueing, lane
+// planning, pageable gathers) proceeds side by side. Rethrows the first error.
+template <class F>
+void for_each_shard(msha_ctx* ctx, F&& f) {
+  const uint32_t k = (uint32_t)ctx->devs.size();
+  if (k == 1) {
+    f(0u);
+    return;
+  }
+  const unsigned per = std::max(1u, std::min(16u, std::max(1u, std::thread::hardware_concurrency())) / k);
+  for (Device& d : ctx->devs)
+    if (!d.gather_pool || d.gather_pool->size() != per) d.gather_pool.reset(new WorkerPool(per - 1));
+  std::vector<std::exception_ptr> errs(k);
+  std::vector<std::thread> th;
+  for (uint32_t s = 0; s < k; ++s)
+    th.emplace_back([&, s] {
+      tl_pool = ctx->devs[s].gather_pool.get();
+      try {
+        f(s);
+      } catch (...) {
+        errs[s] = std::current_exception();
+      }
+      tl_pool = nullptr;
+    });
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
 }
 
 // Device entry points: the context's first device, its error word zeroed once.
@@ -862,12 +900,12 @@ void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* o
                          const uint64_t* len, const uint8_t* arena, uint64_t* bounds) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   partition(len, n, k, bounds);
-  for (uint32_t s = 0; s < k; ++s) {
+  for_each_shard(ctx, [&](uint32_t s) {
     Device& d = ctx->devs[s];
     const uint64_t a = bounds[s], b = bounds[s + 1];
     d.arena_bytes = 0;
     d.st.h2d_payload_bytes = 0;
-    if (a == b) continue;
+    if (a == b) return;
     const unsigned T = plan_threads(b - a);
     std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
     parallel_chunks(b - a, T, [&](unsigned t, uint64_t x, uint64_t y) {
@@ -938,7 +976,7 @@ void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* o
     }
     for (; c < chunks; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
     d.st.h2d_payload_bytes = uploaded;
-  }
+  });
   trace("direct ranges queued", t0);
 }
 
@@ -983,19 +1021,17 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     st.device = ctx->devs[s].id;
     st.h2d_payload_bytes = payload;
   }
-  // uid -> first shard-local message with that payload (UINT64_MAX = none
-  // yet); only needed to find representatives per shard when k > 1
-  std::vector<uint64_t>& placed = ctx->placed;
-  if (uid && k > 1 && placed.size() < n) placed.assign(n, UINT64_MAX);
-  std::vector<uint64_t> touched;  // uids seen in the current shard (reset per shard)
   for (uint32_t s = 0; s < k; ++s) {
+    ctx->devs[s].lo = bounds[s];
+    ctx->devs[s].hi = bounds[s + 1];
+  }
+  // Plan every shard (several GPUs: side by side, for_each_shard).
+  for_each_shard(ctx, [&](uint32_t s) {
     Device& d = ctx->devs[s];
     Plan& P = plans[s];
-    d.lo = bounds[s];
-    d.hi = bounds[s + 1];
     P.m = d.hi - d.lo;
     d.st.messages = P.m;
-    if (P.m == 0) continue;
+    if (P.m == 0) return;
     const uint64_t* L = len + d.lo;
     // Aliases (same uid) have identical bytes, hence identical digests: only
     // the first message of each uid gets a lane; the others copy its digest
@@ -1043,20 +1079,16 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       });
       P.lanes = 0;
       for (uint64_t c : nl) P.lanes += c;
+      uint64_t ncross = 0;
+      for (const std::vector<uint32_t>& v : cross) ncross += v.size();
+      std::unordered_map<uint64_t, uint32_t> first;  // uid -> the shard's first message with it
+      first.reserve(std::min<uint64_t>(ncross, 1u << 16));
       for (const std::vector<uint32_t>& v : cross)
         for (uint32_t i : v) {
-          uint64_t& first = placed[uid[d.lo + i]];
-          if (first == UINT64_MAX) {
-            first = i;
-            touched.push_back(uid[d.lo + i]);
-            P.rep[i] = i;
-            ++P.lanes;
-          } else {
-            P.rep[i] = (uint32_t)first;
-          }
+          const auto it = first.try_emplace(uid[d.lo + i], i);
+          P.rep[i] = it.first->second;
+          P.lanes += it.second;
         }
-      for (uint64_t t : touched) placed[t] = UINT64_MAX;
-      touched.clear();
       if (P.lanes == P.m) P.rep.clear();
     }
     d.st.lanes = P.lanes;
@@ -1068,11 +1100,11 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (direct) {
       // direct mode orders the lanes and fills their metadata in one pass (below)
     } else if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
-      order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp, P.rep.data());
+      order_by_blocks_desc(L, P.m, P.perm.data(), d.sort_tmp, P.rep.data());
       P.ordered = true;
     } else {
       P.ordered = !all_equal_blocks(L, P.m);
-      if (P.ordered) order_by_blocks_desc(L, P.m, P.perm.data(), ctx->sort_tmp);
+      if (P.ordered) order_by_blocks_desc(L, P.m, P.perm.data(), d.sort_tmp);
       else for (uint64_t i = 0; i < P.m; ++i) P.perm[i] = (uint32_t)i;
     }
     trace("lane order", t0);
@@ -1081,7 +1113,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     // reads bytes uploaded by the end of chunk c.
     uint64_t acc = 0;
     if (direct) {  // the shard's byte ranges of the caller's pinned arena, uploaded as is
-      plan_direct_lanes(P, d, direct->off + d.lo, L, h_off, h_len, ctx->tmp_dev);
+      plan_direct_lanes(P, d, direct->off + d.lo, L, h_off, h_len, d.tmp_dev);
       acc = d.arena_bytes;
     } else {
       // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
@@ -1149,7 +1181,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     HIPCHK(hipEventRecord(d.ev0, d.stream));
     HIPCHK(hipEventRecord(d.slot_free[0], d.copy_stream));
     HIPCHK(hipEventRecord(d.slot_free[1], d.copy_stream));
-  }
+  });
   const double t_plan = now_ms();
   trace("planned (metadata H2D queued)", t0);
 
@@ -1223,24 +1255,10 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     // Pageable arenas over several GPUs: one issuing thread per GPU, each with
     // its own gather helpers, so the host copy for GPU s+1 never waits on GPU
     // s's staging slot (msha_shard_stats gather_begin/end show the overlap).
-    const unsigned per = std::max(1u, std::min(16u, std::max(1u, std::thread::hardware_concurrency())) / k);
-    std::vector<std::exception_ptr> errs(k);
-    std::vector<std::thread> th;
-    for (uint32_t s = 0; s < k; ++s) {
-      Device& d = ctx->devs[s];
-      if (!d.gather_pool || d.gather_pool->size() != per) d.gather_pool.reset(new WorkerPool(per - 1));
-      th.emplace_back([&, s] {
-        try {
-          while (issue_chunk(s, *ctx->devs[s].gather_pool)) {
-          }
-        } catch (...) {
-          errs[s] = std::current_exception();
-        }
-      });
-    }
-    for (auto& t : th) t.join();
-    for (auto& e : errs)
-      if (e) std::rethrow_exception(e);
+    for_each_shard(ctx, [&](uint32_t s) {
+      while (issue_chunk(s, cur_pool())) {
+      }
+    });
   } else {
     // One issuing thread, chunks round-robin over the GPUs so every copy
     // engine stays busy (direct mode only enqueues waits and launches here).
