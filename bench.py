@@ -175,7 +175,7 @@ def cpu_baseline(w, seconds: float):
     return line
 
 
-PMC_FILE = "profiles/r01_pmc.json"          # tools/pmc_valu.sh -> tools/pmc_summary.py
+PMC_FILE = "profiles/r02_pmc.json"          # tools/pmc_valu.sh -> tools/pmc_summary.py
 TRAFFIC_FILE = "profiles/r01_traffic.json"  # tools/pmc_traffic.sh (first collection)
 
 

@@ -406,11 +406,11 @@ __device__ __forceinline__ void dod_pair_block(const uint4* tab, const uint32_t*
                                                uint32_t (&w)[16]) {
   dod_pair_words(tab, idx[k], idx[k + 1], w);
 }
-// The final block: the odd digest left (k < cnt), 0x80, zeros, the bit length.
-__device__ __forceinline__ void dod_final_block(const uint4* tab, const uint32_t* idx, uint64_t k,
-                                                uint64_t cnt, uint32_t (&w)[16]) {
-  if (k < cnt) {  // one digest left: 32 bytes + 0x80 + zeros + length fit one block
-    const uint4* d0 = tab + 2 * (uint64_t)idx[k];
+// The final block: the odd digest left (has_one: row i0), 0x80, zeros, the bit length.
+__device__ __forceinline__ void dod_final_words(const uint4* tab, uint32_t i0, bool has_one, uint64_t cnt,
+                                                uint32_t (&w)[16]) {
+  if (has_one) {  // one digest left: 32 bytes + 0x80 + zeros + length fit one block
+    const uint4* d0 = tab + 2 * (uint64_t)i0;
     uint4 v0 = d0[0], v1 = d0[1];
     w[0] = bswap(v0.x); w[1] = bswap(v0.y); w[2] = bswap(v0.z); w[3] = bswap(v0.w);
     w[4] = bswap(v1.x); w[5] = bswap(v1.y); w[6] = bswap(v1.z); w[7] = bswap(v1.w);
@@ -426,12 +426,18 @@ __device__ __forceinline__ void dod_final_block(const uint4* tab, const uint32_t
   w[14] = (uint32_t)(bits >> 32);
   w[15] = (uint32_t)bits;
 }
+__device__ __forceinline__ void dod_final_block(const uint4* tab, const uint32_t* idx, uint64_t k,
+                                                uint64_t cnt, uint32_t (&w)[16]) {
+  dod_final_words(tab, k < cnt ? idx[k] : 0u, k < cnt, cnt, w);
+}
 
 struct DigestSrc {
   // Occupancy hint: the paired digest loads hold a second block (16 VGPRs) while
-  // the first is compressed, ~70 VGPRs. 6 waves per SIMD still hide the loads
-  // (the compression loop's issue rate is flat from 2 to 8 waves).
-  static constexpr int kMinWaves = 6;
+  // the first is compressed, and full() has an LDS-staged and a direct index
+  // path: ~95 VGPRs in the split kernel, so 5 waves per SIMD (the LDS staging
+  // allows 6). That still hides the loads: the compression loop's issue rate is
+  // flat from 2 to 8 waves, and Batch launches run ~3 per SIMD.
+  static constexpr int kMinWaves = 5;
   const uint8_t* table;
   const uint32_t* idx;
   const uint64_t* begin;
@@ -441,13 +447,9 @@ struct DigestSrc {
     uint32_t nb;
     bool ok;
   };
-  template <int MODE>
-  __device__ __forceinline__ void full(uint64_t i, uint8_t* out) const {
-    const uint64_t k0 = begin[i], cnt = begin[i + 1] - k0;
-    const uint4* tab = reinterpret_cast<const uint4*>(table);
-    const uint32_t* ix = idx + k0;
-    State s;
-    state_init(s);
+  // One Batch digest from its part indices, ix(k) = the k-th part's table row.
+  template <class Ix>
+  __device__ __forceinline__ void digest(const uint4* tab, Ix ix, uint64_t cnt, State& s) const {
     uint32_t w[16], nx[16];
     uint64_t k = 0;
     // Two blocks (four digests) per step, all requested before the first is
@@ -456,15 +458,15 @@ struct DigestSrc {
     // instead of being evicted between two half-line requests a block apart
     // (1.57x the algorithmic bytes before, profiles/r01_pmc.json).
     for (; k + 4 <= cnt; k += 4) {
-      dod_pair_block(tab, ix, k, w);
-      dod_pair_block(tab, ix, k + 2, nx);
+      dod_pair_words(tab, ix(k), ix(k + 1), w);
+      dod_pair_words(tab, ix(k + 2), ix(k + 3), nx);
 #pragma unroll
       for (int j = 0; j < 16; ++j) asm volatile("" : "+v"(nx[j]));  // keep the second load here
       compress(s, w);
       compress(s, nx);
     }
     if (k + 2 <= cnt) {
-      dod_pair_block(tab, idx + k0, k, w);
+      dod_pair_words(tab, ix(k), ix(k + 1), w);
       compress(s, w);
       k += 2;
     }
@@ -478,8 +480,57 @@ struct DigestSrc {
       const uint64_t bits = 256 * cnt0;
       compress_uniform_pad(s, 0x80000000u, (uint32_t)(bits >> 32), (uint32_t)bits);
     } else {
-      dod_final_block(tab, idx + k0, k, cnt, w);
+      dod_final_words(tab, k < cnt ? ix(k) : 0u, k < cnt, cnt, w);
       compress(s, w);
+    }
+  }
+  // Part indices staged per wave in LDS: a wave's lanes are consecutive Batches,
+  // so their index lists form one contiguous span of idx, copied once with
+  // coalesced loads; each lane then reads its indices from LDS. Read straight
+  // from idx, a wave's 64 index lists (80 B each for BatchSize 20) were fetched
+  // from L2/MALL again at every step (c3dd 1.12x its algorithmic bytes). Spans
+  // over kIdxStage / 64 indices per active lane read idx directly.
+  static constexpr uint32_t kIdxStage = 1536;  // 6 KiB per wave, 24 KiB per workgroup
+  template <int MODE>
+  __device__ __forceinline__ void full(uint64_t i, uint8_t* out) const {
+    __shared__ uint32_t sidx[4][kIdxStage];
+    const uint64_t k0 = begin[i], k1 = begin[i + 1], cnt = k1 - k0;
+    const uint4* tab = reinterpret_cast<const uint4*>(table);
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    // the active lanes are a prefix of the wave (messages past n returned)
+    const uint32_t act = (uint32_t)__popcll(__ballot(1));
+    const uint64_t s0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(k0 >> 32)) << 32) |
+                        __builtin_amdgcn_readfirstlane((uint32_t)k0);
+    const uint64_t s1 = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(k1 >> 32), act - 1) << 32) |
+                        __builtin_amdgcn_readlane((uint32_t)k1, act - 1);
+    State s;
+    state_init(s);
+    constexpr int kPer = kIdxStage / 64;  // staged indices per lane
+    if (s1 - s0 <= (uint64_t)kPer * act) {
+      uint32_t* st = sidx[wv];
+      const uint32_t span = (uint32_t)(s1 - s0);
+      // all of a lane's share in flight at once (kPer loads; a dependent
+      // load -> store per element would serialize ~20 HBM latencies before the
+      // first block)
+      uint32_t v[kPer];
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) {
+        const uint32_t j = r * act + lane;
+        v[r] = j < span ? idx[s0 + j] : 0u;
+      }
+#pragma unroll
+      for (int r = 0; r < kPer; ++r) {
+        const uint32_t j = r * act + lane;
+        if (j < span) st[j] = v[r];
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      const uint32_t base = (uint32_t)(k0 - s0);
+      digest(tab, [&](uint64_t k) { return st[base + (uint32_t)k]; }, cnt, s);
+    } else {
+      const uint32_t* ix = idx + k0;
+      digest(tab, [&](uint64_t k) { return ix[k]; }, cnt, s);
     }
     store_digest(s, out + 32 * i);
   }

@@ -16,7 +16,7 @@ if [[ $STEPS == all || $STEPS == *smoke* ]]; then
 fi
 if [[ $STEPS == all || $STEPS == *bench* ]]; then
   for cfg in ${CONFIGS:-c2 c3 c3dd c4 c5}; do
-    extra="--no-cpu-baseline"; [ $cfg == c2 ] && extra=""
+    extra="--no-extra"; [ $cfg == c2 ] && extra=""
     timeout -k 10 400 python bench.py --config $cfg ${BSTEPS:+--steps $BSTEPS} $extra > gpurun_out/bench_$cfg.json 2> gpurun_out/bench_$cfg.err; stop_on_fault $? bench_$cfg
     cat gpurun_out/bench_$cfg.json
   done
