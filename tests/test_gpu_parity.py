@@ -634,3 +634,40 @@ def test_pageable_gather_runs_per_shard_in_parallel(monkeypatch):
         assert max(s["gather_begin_ms"] for s in sh) < min(s["gather_end_ms"] for s in sh), sh
         assert sum(s["h2d_payload_bytes"] for s in sh) == int(w.len.sum())
         assert sum(s["launches"] for s in sh) >= 2
+
+
+@pytest.mark.parametrize("shards", [1, 2])
+def test_concurrent_contexts_on_threads(monkeypatch, shards):
+    """mirsha.h: distinct contexts may be used concurrently. Two Python threads
+    (ctypes drops the GIL in the call), each with its own context, hash different
+    batches at the same time through the host API -- with aliases and mixed sizes,
+    pinned and pageable arenas, one and two shards per context -- every digest right."""
+    import threading
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", str(shards))
+    wa = W.c5_storm(1 << 16)
+    wb = W.c2_requests(1 << 17)
+    exp = {"a": _oracle_dedup(wa), "b": oracle.digest_batch(wb.arena, wb.off, wb.len)}
+    got, errs = {}, []
+
+    def run(tag, w, pinned):
+        try:
+            with Engine(1) as e:
+                arena = w.arena
+                if pinned:
+                    arena = e.pinned_empty(w.arena.size)
+                    arena[:] = w.arena
+                for _ in range(3):
+                    got[tag] = e.digest_batch(arena, w.off, w.len)
+                    if not np.array_equal(got[tag], exp[tag]):
+                        errs.append(tag)
+        except Exception as ex:  # surfaced below
+            errs.append(repr(ex))
+
+    th = [threading.Thread(target=run, args=("a", wa, True)), threading.Thread(target=run, args=("b", wb, False))]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+    assert set(got) == {"a", "b"}
