@@ -189,28 +189,33 @@ __device__ __forceinline__ void hash_message_pipe(const uint8_t* p, uint64_t len
   if (nfull == 0) {
     load_block16(p, tail);
   } else {
-    uint32_t A[64], B[64], rawX[16], rawY[16];
-    load_block16(p, rawX);
-    expand_block(rawX, A);
-    load_block16(blk(1), rawX);
+    // Raw block buffers X, Y, Z, V rotate over four steps; each pair of blocks
+    // (b+2, b+3 with b even) is requested together, both halves of a 128-byte
+    // line back to back, so the line is read from HBM once (one block per
+    // request read c4's lines twice: 1.14x the algorithmic bytes).
+    uint32_t A[64], B[64], X[16], Y[16], Z[16], V[16];
+    load_block16(p, X);
+    expand_block(X, A);
+    load_block16(blk(1), X);
     uint32_t b = 0;
+    auto take = [&](const uint32_t (&src)[16]) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) tail[j] = src[j];
+    };
     for (;;) {
-      // A = schedule of block b, rawX = bytes of block b+1 (clamped)
-      load_block16(blk(b + 2), rawY);
-      rounds_expand(s, A, B, rawX);
-      if (++b >= nfull) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) tail[j] = rawX[j];
-        break;
-      }
-      // B = schedule of block b, rawY = bytes of block b+1 (clamped)
-      load_block16(blk(b + 2), rawX);
-      rounds_expand(s, B, A, rawY);
-      if (++b >= nfull) {
-#pragma unroll
-        for (int j = 0; j < 16; ++j) tail[j] = rawY[j];
-        break;
-      }
+      // A = schedule of block b (b % 4 == 0), X = bytes of block b+1 (clamped)
+      load_block16(blk(b + 2), Y);
+      load_block16(blk(b + 3), Z);
+      rounds_expand(s, A, B, X);
+      if (++b >= nfull) { take(X); break; }
+      rounds_expand(s, B, A, Y);  // B = block b, Y = block b+1
+      if (++b >= nfull) { take(Y); break; }
+      load_block16(blk(b + 2), V);
+      load_block16(blk(b + 3), X);
+      rounds_expand(s, A, B, Z);  // A = block b, Z = block b+1
+      if (++b >= nfull) { take(Z); break; }
+      rounds_expand(s, B, A, V);  // B = block b, V = block b+1
+      if (++b >= nfull) { take(V); break; }
     }
   }
   uint32_t w[16];

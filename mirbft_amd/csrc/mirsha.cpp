@@ -1274,7 +1274,10 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     HIPCHK(hipSetDevice(d.id));
     HIPCHK(hipEventRecord(d.ev1, d.stream));
     if (!plans[s].identity()) {
-      HIPCHK(hipMemcpyAsync(d.h_out.p, d.out.p, 32 * m, hipMemcpyDeviceToHost, d.stream));
+      // d.out is message-ordered (lane q wrote slot perm[q]); a pinned result
+      // buffer takes it as is, the aliases' slots are filled on the host below
+      HIPCHK(hipMemcpyAsync(out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>(), d.out.p, 32 * m,
+                            hipMemcpyDeviceToHost, d.stream));
       d.st.d2h_bytes += 32 * m;
     }
     HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
@@ -1295,7 +1298,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     kernel_ms = std::max<double>(kernel_ms, ms);
     uint32_t errflag;
     std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
-    const bool straight = P.identity() && out_pinned;  // identity digests were D2H'd straight into out
+    const bool straight = out_pinned;  // the digests were D2H'd straight into out
     if (errflag & 2) {
       // a split chain's handoff timed out: its digests are undefined; the
       // payload is still on the device, so re-hash the shard unsplit
@@ -1311,7 +1314,15 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     gather_ms += d.st.gather_ms;
     const std::vector<uint32_t>& rep = P.rep;
     const uint8_t* h = d.h_out.as<uint8_t>();
-    if (straight) continue;
+    if (straight) {
+      if (!rep.empty())  // aliases copy their representative's digest
+        parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
+          uint8_t* o = out + 32 * d.lo;
+          for (uint64_t i = a; i < b; ++i)
+            if (rep[i] != i) std::memcpy(o + 32 * i, o + 32 * (uint64_t)rep[i], 32);
+        });
+      continue;
+    }
     parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
       if (rep.empty())
         std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));
