@@ -16,10 +16,12 @@ So a log recorded by the reference on a Go-equipped box is a set of golden
 pairs from the real protocol: ``verify_trace`` re-hashes every reconstructed
 input on the GPU (one batch) and compares with the recorded digests.
 
-Protobuf wire format is decoded by hand (no protoc in this image); only the
-fields on the hash path are interpreted, every other field is skipped.
-Field numbers: protos/recording/recording.proto:14-18,
-protos/state/state.proto:16-31,78-109, protos/msgs/msgs.proto:231-235,255-289.
+Protobuf wire format is decoded by hand (no protoc in this image) against
+``SCHEMA``, the field tables of the messages on the hash path; every other field
+is skipped. ``SCHEMA`` is pinned to the reference's own generated descriptors
+(``pkg/pb/*/*.pb.go`` raw descriptors -> tests/golden/eventlog_schema.json), and
+the official protobuf runtime, driven by those descriptors, encodes the events
+the tests decode.
 """
 from __future__ import annotations
 
@@ -106,16 +108,88 @@ def _read_varint_signed(stream: io.BufferedReader) -> Optional[int]:
     return (x >> 1) ^ -(x & 1)
 
 
-def _msg(fn: int, payload: bytes) -> bytes:
-    return _put_uvarint(fn << 3 | 2) + _put_uvarint(len(payload)) + payload
+# ---------------------------------------------------------------------------
+# the schema of the hash path
+# ---------------------------------------------------------------------------
+# message -> {field number: (field name, kind, repeated)}; kind is "uint64",
+# "int64", "bytes" or a message name. Restates the field tables of
+# protos/recording/recording.proto:14-18, protos/state/state.proto:16-31,78-109
+# and protos/msgs/msgs.proto:231-235,255-289 for the messages a HashResult passes
+# through. tests/test_eventlog.py checks every entry against the reference's
+# generated descriptors (tests/golden/eventlog_schema.json).
+SCHEMA: Dict[str, Dict[int, Tuple[str, str, bool]]] = {
+    "recording.Event": {1: ("node_id", "uint64", False), 2: ("time", "int64", False),
+                        3: ("state_event", "state.Event", False)},
+    "state.Event": {4: ("hash_result", "state.EventHashResult", False),
+                    10: ("tick_elapsed", "state.EventTickElapsed", False)},
+    "state.EventTickElapsed": {},
+    "state.EventHashResult": {1: ("digest", "bytes", False), 2: ("origin", "state.HashOrigin", False)},
+    "state.HashOrigin": {1: ("batch", "state.HashOrigin.Batch", False),
+                         2: ("epoch_change", "state.HashOrigin.EpochChange", False),
+                         3: ("verify_batch", "state.HashOrigin.VerifyBatch", False)},
+    "state.HashOrigin.Batch": {1: ("source", "uint64", False), 2: ("epoch", "uint64", False),
+                               3: ("seq_no", "uint64", False), 5: ("request_acks", "msgs.RequestAck", True)},
+    "state.HashOrigin.EpochChange": {1: ("source", "uint64", False), 2: ("origin", "uint64", False),
+                                     3: ("epoch_change", "msgs.EpochChange", False)},
+    "state.HashOrigin.VerifyBatch": {1: ("source", "uint64", False), 2: ("seq_no", "uint64", False),
+                                     3: ("request_acks", "msgs.RequestAck", True),
+                                     4: ("expected_digest", "bytes", False)},
+    "msgs.RequestAck": {1: ("client_id", "uint64", False), 2: ("req_no", "uint64", False),
+                        3: ("digest", "bytes", False)},
+    "msgs.Checkpoint": {1: ("seq_no", "uint64", False), 2: ("value", "bytes", False)},
+    "msgs.EpochChange": {1: ("new_epoch", "uint64", False), 2: ("checkpoints", "msgs.Checkpoint", True),
+                         3: ("p_set", "msgs.EpochChange.SetEntry", True),
+                         4: ("q_set", "msgs.EpochChange.SetEntry", True)},
+    "msgs.EpochChange.SetEntry": {1: ("epoch", "uint64", False), 2: ("seq_no", "uint64", False),
+                                  3: ("digest", "bytes", False)},
+}
+
+# state.Event's oneof members by field number (state.proto:16-31): RecordedEvent.kind.
+EVENT_KINDS = {1: "initialize", 2: "load_persisted_entry", 3: "complete_initialization", 4: "hash_result",
+               5: "checkpoint_result", 6: "request_persisted", 7: "state_transfer_complete",
+               8: "state_transfer_failed", 9: "step", 10: "tick_elapsed", 11: "actions_received"}
+
+_SCALAR_WIRE = {"uint64": 0, "int64": 0, "bytes": 2}
 
 
-def _u64(fn: int, v: int) -> bytes:
-    return b"" if v == 0 else _put_uvarint(fn << 3) + _put_uvarint(v & 0xFFFFFFFFFFFFFFFF)
+def _decode(buf: bytes, name: str) -> dict:
+    """One message as {field name: value}; unknown fields are skipped (proto3)."""
+    spec = SCHEMA[name]
+    out: dict = {}
+    for fn, wt, v in _fields(buf):
+        if fn not in spec:
+            continue
+        fname, kind, rep = spec[fn]
+        if wt != _SCALAR_WIRE.get(kind, 2):
+            raise EventLogError(f"{name}.{fname}: wire type {wt}")
+        if kind == "int64":
+            v = v - (1 << 64) if v >= 1 << 63 else v
+        elif kind in SCHEMA:
+            v = _decode(v, kind)
+        if rep:
+            out.setdefault(fname, []).append(v)
+        else:
+            out[fname] = v      # last one wins, as in proto3
+    return out
 
 
-def _bytes(fn: int, v: bytes) -> bytes:
-    return b"" if not v else _msg(fn, v)
+def _encode(name: str, msg: dict) -> bytes:
+    """Inverse of _decode: fields in number order, zero scalars omitted (what
+    Go's proto.Marshal writes for these proto3 messages)."""
+    out = bytearray()
+    for fn, (fname, kind, rep) in sorted(SCHEMA[name].items()):
+        v = msg.get(fname)
+        for x in (v or []) if rep else ([] if v is None else [v]):
+            if kind in ("uint64", "int64"):
+                if x:
+                    out += _put_uvarint(fn << 3) + _put_uvarint(x & 0xFFFFFFFFFFFFFFFF)
+            elif kind == "bytes":
+                if x:
+                    out += _put_uvarint(fn << 3 | 2) + _put_uvarint(len(x)) + x
+            else:
+                body = _encode(kind, x)
+                out += _put_uvarint(fn << 3 | 2) + _put_uvarint(len(body)) + body
+    return bytes(out)
 
 
 # ---------------------------------------------------------------------------
@@ -144,91 +218,56 @@ class HashResultEvent:
 class RecordedEvent:
     node_id: int
     time: int
-    kind: int                       # state.Event oneof field number (4 = hash_result, 10 = tick_elapsed, ...)
+    kind: int                       # state.Event oneof field number (EVENT_KINDS: 4 = hash_result, 10 = tick_elapsed)
     hash_result: Optional[HashResultEvent] = None
 
-
-def _request_ack(b: bytes) -> RequestAck:
-    c = r = 0
-    d = b""
-    for fn, _, v in _fields(b):
-        if fn == 1: c = v
-        elif fn == 2: r = v
-        elif fn == 3: d = v
-    return RequestAck(c, r, d)
+    @property
+    def kind_name(self) -> str:
+        return EVENT_KINDS.get(self.kind, f"unknown({self.kind})")
 
 
-def _epoch_change(b: bytes) -> EpochChange:
-    ec = EpochChange(new_epoch=0)
-    for fn, _, v in _fields(b):
-        if fn == 1:
-            ec.new_epoch = v
-        elif fn == 2:
-            sq, val = 0, b""
-            for f2, _, v2 in _fields(v):
-                if f2 == 1: sq = v2
-                elif f2 == 2: val = v2
-            ec.checkpoints.append(Checkpoint(sq, val))
-        elif fn in (3, 4):
-            ep = sq = 0
-            dg = b""
-            for f2, _, v2 in _fields(v):
-                if f2 == 1: ep = v2
-                elif f2 == 2: sq = v2
-                elif f2 == 3: dg = v2
-            (ec.p_set if fn == 3 else ec.q_set).append(SetEntry(ep, sq, dg))
-    return ec
+def _acks(ms: List[dict]) -> List[RequestAck]:
+    return [RequestAck(a.get("client_id", 0), a.get("req_no", 0), a.get("digest", b"")) for a in ms]
 
 
-def _hash_origin(b: bytes) -> HashOrigin:
-    for fn, _, v in _fields(b):
-        if fn == 1:     # Batch{source=1, epoch=2, seq_no=3, request_acks=5}
-            o = HashOriginBatch(0, 0, 0)
-            for f2, _, v2 in _fields(v):
-                if f2 == 1: o.source = v2
-                elif f2 == 2: o.epoch = v2
-                elif f2 == 3: o.seq_no = v2
-                elif f2 == 5: o.request_acks.append(_request_ack(v2))
-            return HashOrigin(o)
-        if fn == 2:     # EpochChange{source=1, origin=2, epoch_change=3}
-            o = HashOriginEpochChange(0, 0, None)
-            for f2, _, v2 in _fields(v):
-                if f2 == 1: o.source = v2
-                elif f2 == 2: o.origin = v2
-                elif f2 == 3: o.epoch_change = _epoch_change(v2)
-            return HashOrigin(o)
-        if fn == 3:     # VerifyBatch{source=1, seq_no=2, request_acks=3, expected_digest=4}
-            o = HashOriginVerifyBatch(0, 0)
-            for f2, _, v2 in _fields(v):
-                if f2 == 1: o.source = v2
-                elif f2 == 2: o.seq_no = v2
-                elif f2 == 3: o.request_acks.append(_request_ack(v2))
-                elif f2 == 4: o.expected_digest = v2
-            return HashOrigin(o)
+def _epoch_change(m: dict) -> EpochChange:
+    sets = lambda k: [SetEntry(e.get("epoch", 0), e.get("seq_no", 0), e.get("digest", b"")) for e in m.get(k, [])]
+    return EpochChange(new_epoch=m.get("new_epoch", 0),
+                       checkpoints=[Checkpoint(c.get("seq_no", 0), c.get("value", b""))
+                                    for c in m.get("checkpoints", [])],
+                       p_set=sets("p_set"), q_set=sets("q_set"))
+
+
+def _hash_origin(m: dict) -> HashOrigin:
+    if "batch" in m:
+        b = m["batch"]
+        return HashOrigin(HashOriginBatch(b.get("source", 0), b.get("epoch", 0), b.get("seq_no", 0),
+                                          _acks(b.get("request_acks", []))))
+    if "epoch_change" in m:
+        e = m["epoch_change"]
+        ec = e.get("epoch_change")
+        return HashOrigin(HashOriginEpochChange(e.get("source", 0), e.get("origin", 0),
+                                                None if ec is None else _epoch_change(ec)))
+    if "verify_batch" in m:
+        v = m["verify_batch"]
+        return HashOrigin(HashOriginVerifyBatch(v.get("source", 0), v.get("seq_no", 0),
+                                                _acks(v.get("request_acks", [])), v.get("expected_digest", b"")))
     return HashOrigin(None)
 
 
 def decode_event(b: bytes) -> RecordedEvent:
-    node_id = time = 0
+    """One recording.Event (recording.proto:14-18)."""
+    m = _decode(b, "recording.Event")
     kind = 0
-    hr = None
-    for fn, _, v in _fields(b):
-        if fn == 1:
-            node_id = v
-        elif fn == 2:
-            time = v - (1 << 64) if v >= 1 << 63 else v  # int64
-        elif fn == 3:
-            for f2, _, v2 in _fields(v):
+    for fn, _, v in _fields(b):          # which state.Event oneof member is set (any, known or not)
+        if fn == 3:
+            for f2, _, _ in _fields(v):
                 kind = f2
-                if f2 == 4:  # EventHashResult{digest=1, origin=2}
-                    dg, org = b"", HashOrigin(None)
-                    for f3, _, v3 in _fields(v2):
-                        if f3 == 1: dg = v3
-                        elif f3 == 2: org = _hash_origin(v3)
-                    hr = (dg, org)
-    ev = RecordedEvent(node_id, time, kind)
+    ev = RecordedEvent(m.get("node_id", 0), m.get("time", 0), kind)
+    hr = m.get("state_event", {}).get("hash_result")
     if hr is not None:
-        ev.hash_result = HashResultEvent(node_id, time, hr[0], hr[1])
+        ev.hash_result = HashResultEvent(ev.node_id, ev.time, hr.get("digest", b""),
+                                         _hash_origin(hr.get("origin", {})))
     return ev
 
 
@@ -262,50 +301,42 @@ def read_events(source: Union[str, bytes, io.IOBase]) -> Iterator[RecordedEvent]
 # ---------------------------------------------------------------------------
 # encoder (fixtures, round-trip tests)
 # ---------------------------------------------------------------------------
-def _enc_ack(a: RequestAck) -> bytes:
-    return _u64(1, a.client_id) + _u64(2, a.req_no) + _bytes(3, a.digest)
+def _ack_msg(a: RequestAck) -> dict:
+    return {"client_id": a.client_id, "req_no": a.req_no, "digest": a.digest}
 
 
-def _enc_epoch_change(ec: EpochChange) -> bytes:
-    out = _u64(1, ec.new_epoch)
-    for cp in ec.checkpoints:
-        out += _msg(2, _u64(1, cp.seq_no) + _bytes(2, cp.value))
-    for fn, s in ((3, ec.p_set), (4, ec.q_set)):
-        for e in s:
-            out += _msg(fn, _u64(1, e.epoch) + _u64(2, e.seq_no) + _bytes(3, e.digest))
-    return out
-
-
-def _enc_origin(o: HashOrigin) -> bytes:
+def _origin_msg(o: HashOrigin) -> dict:
     t = o.type
     if isinstance(t, HashOriginBatch):
-        body = _u64(1, t.source) + _u64(2, t.epoch) + _u64(3, t.seq_no)
-        for a in t.request_acks:
-            body += _msg(5, _enc_ack(a))
-        return _msg(1, body)
+        return {"batch": {"source": t.source, "epoch": t.epoch, "seq_no": t.seq_no,
+                          "request_acks": [_ack_msg(a) for a in t.request_acks]}}
     if isinstance(t, HashOriginEpochChange):
-        body = _u64(1, t.source) + _u64(2, t.origin)
-        if t.epoch_change is not None:
-            body += _msg(3, _enc_epoch_change(t.epoch_change))
-        return _msg(2, body)
+        m = {"source": t.source, "origin": t.origin}
+        ec = t.epoch_change
+        if ec is not None:
+            m["epoch_change"] = {
+                "new_epoch": ec.new_epoch,
+                "checkpoints": [{"seq_no": c.seq_no, "value": c.value} for c in ec.checkpoints],
+                "p_set": [{"epoch": e.epoch, "seq_no": e.seq_no, "digest": e.digest} for e in ec.p_set],
+                "q_set": [{"epoch": e.epoch, "seq_no": e.seq_no, "digest": e.digest} for e in ec.q_set]}
+        return {"epoch_change": m}
     if isinstance(t, HashOriginVerifyBatch):
-        body = _u64(1, t.source) + _u64(2, t.seq_no)
-        for a in t.request_acks:
-            body += _msg(3, _enc_ack(a))
-        return _msg(3, body + _bytes(4, t.expected_digest))
-    return b""
+        return {"verify_batch": {"source": t.source, "seq_no": t.seq_no,
+                                 "request_acks": [_ack_msg(a) for a in t.request_acks],
+                                 "expected_digest": t.expected_digest}}
+    return {}
 
 
 def encode_event(node_id: int, time: int, hash_result: Optional[Tuple[bytes, HashOrigin]] = None,
                  tick: bool = False) -> bytes:
     """recording.Event{node_id, time, state_event} with a HashResult or a TickElapsed."""
     if hash_result is not None:
-        se = _msg(4, _bytes(1, hash_result[0]) + _msg(2, _enc_origin(hash_result[1])))
+        se = {"hash_result": {"digest": hash_result[0], "origin": _origin_msg(hash_result[1])}}
     elif tick:
-        se = _msg(10, b"")
+        se = {"tick_elapsed": {}}
     else:
         raise ValueError("nothing to encode")
-    return _u64(1, node_id) + _u64(2, time & 0xFFFFFFFFFFFFFFFF) + _msg(3, se)
+    return _encode("recording.Event", {"node_id": node_id, "time": time, "state_event": se})
 
 
 def write_log(records: List[bytes]) -> bytes:
