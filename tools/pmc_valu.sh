@@ -3,6 +3,7 @@
 #   sq    : VALU/SALU instruction counts, VALU-active and wave cycles, waits, clock (GRBM)
 #   sq2   : INT32 VALU instructions, integer ops, VALU thread-cycles, SALU cycles, LDS instrs
 #   fetch : FETCH_SIZE        write : WRITE_SIZE   (HBM bytes, gfx950 recipe)
+#   ifetch: instruction cache (SQC_ICACHE_*), instruction-issue waits, instruction fetches
 # -> gpurun_out/pmc/<cfg>_<pass>/run_counter_collection.csv; summarise with
 #    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc.json
 set -u
@@ -16,14 +17,17 @@ prof() {  # name, counters, cmd...
 }
 SQ="SQ_WAVES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_INSTS_SALU SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_BUSY_CYCLES GRBM_GUI_ACTIVE GRBM_COUNT"
 SQ2="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_IOPS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_SALU SQ_INSTS_LDS GRBM_GUI_ACTIVE"
+IF="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_IFETCH SQ_INSTS_VALU GRBM_GUI_ACTIVE"
 PASSES=${PASSES:-sq sq2 fetch write}
+has() { [[ " $PASSES " == *" $1 "* ]]; }
 for spec in ${SPECS:-c2:auto c3:auto c3dd:auto c4:auto c5:auto ub_16384_65536:coop ub_16384_65536:lane}; do
   cfg=${spec%%:*}; pol=${spec##*:}; arg=$(echo $cfg | tr '_' ':')
   name=${cfg}_${pol}
   cmd="python3 bench.py --config $arg --policy $pol --steps 3 --warmup 1 --no-cpu-baseline --no-extra"
-  [[ $PASSES == *"sq "* || $PASSES == sq ]] && prof ${name}_sq "$SQ" $cmd
-  [[ $PASSES == *sq2* ]] && prof ${name}_sq2 "$SQ2" $cmd
-  [[ $PASSES == *fetch* ]] && prof ${name}_fetch FETCH_SIZE $cmd
-  [[ $PASSES == *write* ]] && prof ${name}_write WRITE_SIZE $cmd
+  has sq && prof ${name}_sq "$SQ" $cmd
+  has sq2 && prof ${name}_sq2 "$SQ2" $cmd
+  has fetch && prof ${name}_fetch FETCH_SIZE $cmd
+  has write && prof ${name}_write WRITE_SIZE $cmd
+  has ifetch && prof ${name}_ifetch "$IF" $cmd
 done
 exit 0
