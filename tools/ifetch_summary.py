@@ -1,3 +1,7 @@
+#!/usr/bin/env python3
+"""Summarise the `ifetch` PMC pass of tools/pmc_valu.sh (instruction cache hits/misses,
+instruction fetches per VALU instruction, share of wave cycles waiting for issue) for the
+last msha kernel dispatch in each run_counter_collection.csv given."""
 import csv,sys,collections
 for f in sys.argv[1:]:
     rows=list(csv.DictReader(open(f)))
