@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 3u
+#define MSHA_ABI_VERSION 4u
 
 enum {
   MSHA_OK = 0,
@@ -83,6 +83,7 @@ typedef struct {
   /* Last host-memory call, summed over GPUs (see msha_get_shard_stats): */
   uint64_t h2d_bytes;       /* payload + metadata uploaded */
   uint64_t d2h_bytes;       /* digests + status words downloaded */
+  uint64_t small_calls;     /* host calls served by the small-call (latency) path: one H2D, one launch, one D2H */
 } msha_stats;
 
 /* Per-GPU figures of the last host-memory call (one entry per shard; a shard is

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -52,6 +52,7 @@ class MshaStats(ctypes.Structure):
         ("split_retries", ctypes.c_uint64),
         ("h2d_bytes", ctypes.c_uint64),
         ("d2h_bytes", ctypes.c_uint64),
+        ("small_calls", ctypes.c_uint64),
     ]
 
 

@@ -204,6 +204,9 @@ struct Device {
   std::vector<hipEvent_t> span_ev;               // direct mode: span chunk c is on the device
   DevBuf arena, off, len, order, out, err, idx, begin, table;
   PinBuf h_arena, h_meta, h_out, slot[2];
+  // small-call path (run_small): [meta | payload] in, [error word | digests] out
+  DevBuf sm_in, sm_out;
+  PinBuf sm_stage, sm_res;
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
@@ -232,10 +235,10 @@ struct Device {
   uint64_t split_epoch = 0;
   void release() {
     gather_pool.reset();
-    for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table}) b->release();
+    for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table, &sm_in, &sm_out}) b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
-    for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1]}) b->release();
+    for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1], &sm_stage, &sm_res}) b->release();
     for (hipEvent_t* e : {&ev0, &ev1, &slot_free[0], &slot_free[1], &chunk_in}) {
       if (*e) (void)hipEventDestroy(*e);
       *e = nullptr;
@@ -998,6 +1001,119 @@ void rerun_unsplit(msha_ctx* ctx, Device& d, const Plan& P, uint8_t* d2h_dst) {
   __atomic_fetch_add(&ctx->stats.split_retries, 1, __ATOMIC_RELAXED);
 }
 
+// ---------------------------------------------------------------------------
+// Small calls: the latency path. MirBFT's hash worker hands over one
+// ActionList per call (mirbft.go:282-302), and at low load that is a handful of
+// actions. run_pipeline's round trip costs ~60-80 us whatever the size (seven
+// queue operations over two streams, events, planning passes), while the GPU
+// floor of H2D + kernel + D2H is ~18 us (tools/op_latency.hip). A call of at
+// most small_msgs() messages and small_bytes() of payload therefore runs on the
+// context's first GPU as: messages packed behind their metadata in one pinned
+// staging buffer -> ONE H2D (a pinned, 16-byte aligned arena span over 512 KiB
+// is uploaded as is instead: metadata H2D + span H2D), one launch, ONE D2H of
+// [error word | digests]. No alias folding (an identical payload is simply hashed again)
+// and no sharding: neither pays at this size. MSHA_SMALL_BYTES (default 1 MiB,
+// 0 disables) and MSHA_SMALL_MSGS (default 4096) set the limits.
+// ---------------------------------------------------------------------------
+uint64_t env_u64(const char* name, uint64_t dflt) {
+  const char* e = getenv(name);
+  return e ? strtoull(e, nullptr, 10) : dflt;
+}
+// read per call (a getenv is ~0.1 us): tests switch paths within one process
+uint64_t small_bytes() { return env_u64("MSHA_SMALL_BYTES", 1ull << 20); }
+uint64_t small_msgs() { return env_u64("MSHA_SMALL_MSGS", 4096); }
+constexpr uint64_t kSmallSpanMin = 512ull << 10;
+inline bool small_call(uint64_t n, uint64_t bytes) {
+  return n <= small_msgs() && bytes <= small_bytes() && small_bytes() > 0;
+}
+
+// The caller's pinned arena, uploaded as is: messages i at base + off[i], all
+// inside [lo, hi), 16-byte aligned.
+struct SmallSpan {
+  const uint8_t* base;
+  const uint64_t* off;
+  uint64_t lo, hi;
+};
+
+template <class Fill>
+void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_t* out, Fill&& fill,
+               const SmallSpan* span = nullptr) {
+  Device& d = ctx->devs[0];
+  const uint64_t meta = (16 * m + 63) & ~uint64_t(63);  // off[m], len[m]; payload 64-B aligned after
+  uint64_t pay = 0;
+  if (span) {
+    pay = span->hi - span->lo;
+  } else {
+    for (uint64_t i = 0; i < m; ++i) pay += round16(len[i]);
+  }
+  d.sm_stage.ensure(meta + (span ? 0 : pay));
+  uint64_t* h_off = d.sm_stage.as<uint64_t>();
+  uint64_t* h_len = h_off + m;
+  uint8_t* h_pay = d.sm_stage.as<uint8_t>() + meta;
+  uint64_t a = 0;
+  for (uint64_t i = 0; i < m; ++i) {
+    h_len[i] = len[i];
+    if (span) {
+      h_off[i] = span->off[i] - span->lo;
+    } else {
+      h_off[i] = a;
+      if (len[i]) fill(i, h_pay + a);
+      a += round16(len[i]);
+    }
+  }
+  const double t_pack = now_ms();
+  HIPCHK(hipSetDevice(d.id));
+  d.sm_in.ensure(meta + pay + msha::kArenaSlack);
+  const uint64_t out_cap = d.sm_out.cap;
+  d.sm_out.ensure(32 + 32 * m);
+  // the error word heads the output buffer; zeroed once per allocation and
+  // again only after a call that found it set
+  if (d.sm_out.cap != out_cap) HIPCHK(hipMemsetAsync(d.sm_out.p, 0, 32, d.stream));
+  d.sm_res.ensure(32 + 32 * m);
+  uint8_t* dev_in = d.sm_in.as<uint8_t>();
+  if (span) {
+    HIPCHK(hipMemcpyAsync(dev_in, h_off, 16 * m, hipMemcpyHostToDevice, d.stream));
+    if (pay) HIPCHK(hipMemcpyAsync(dev_in + meta, span->base + span->lo, pay, hipMemcpyHostToDevice, d.stream));
+  } else {
+    HIPCHK(hipMemcpyAsync(dev_in, h_off, meta + pay, hipMemcpyHostToDevice, d.stream));
+  }
+  msha::LaunchKind kind;
+  HIPCHK(msha::launch_digest_batch(dev_in + meta, reinterpret_cast<const uint64_t*>(dev_in),
+                                   reinterpret_cast<const uint64_t*>(dev_in) + m, nullptr, nullptr, m,
+                                   d.sm_out.as<uint8_t>() + 32, d.sm_out.as<uint32_t>(), d.cus,
+                                   ctx->kernel_policy, d.stream, nullptr, &kind));
+  HIPCHK(hipMemcpyAsync(d.sm_res.p, d.sm_out.p, 32 + 32 * m, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  const double t_dev = now_ms();
+  uint32_t errflag;
+  std::memcpy(&errflag, d.sm_res.p, 4);
+  if (errflag) {  // cannot happen (aligned payloads, no split chains): leave the word clean, report
+    HIPCHK(hipMemsetAsync(d.sm_out.p, 0, 32, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    throw MshaError(MSHA_ERR_HIP, "internal: device error flag " + std::to_string(errflag) + " on a small call");
+  }
+  std::memcpy(out, d.sm_res.as<uint8_t>() + 32, 32 * m);
+  for (Device& o : ctx->devs) {
+    o.st = msha_shard_stats{};
+    o.st.device = o.id;
+  }
+  const uint64_t h2d = 16 * m + (span ? pay : meta - 16 * m + pay);
+  d.st.messages = d.st.lanes = m;
+  d.st.h2d_payload_bytes = pay;
+  d.st.h2d_bytes = h2d;
+  d.st.d2h_bytes = 32 + 32 * m;
+  d.st.device_ms = t_dev - t_pack;
+  count_launch(ctx, &d, kind);
+  ctx->stats.calls++;
+  ctx->stats.small_calls++;
+  ctx->stats.plan_ms = t_pack - t0;
+  ctx->stats.pack_ms = span ? 0 : t_pack - t0;
+  ctx->stats.device_ms = t_dev - t_pack;
+  ctx->stats.h2d_bytes = h2d;
+  ctx->stats.d2h_bytes = 32 + 32 * m;
+  ctx->stats.total_ms = now_ms() - t0;
+}
+
 template <class Gather>
 void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, const uint64_t* uid,
                   uint8_t* out, Gather&& gather, const Direct* direct = nullptr,
@@ -1527,6 +1643,25 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
       offbits |= r.offbits;
     }
     const bool aligned16 = (offbits & 15) == 0;
+    if (n <= small_msgs()) {  // the latency path (run_small)
+      // A pinned arena goes up as is only above 512 KiB: below that, packing it
+      // behind the metadata (one H2D instead of two) is the faster of the two
+      // (tools/latency.cpp: 32 KiB pinned 57 us as two copies, 44 us packed).
+      const bool span = aligned16 && hi - lo > kSmallSpanMin && hi - lo <= small_bytes() &&
+                        is_pinned_host(arena + lo);
+      uint64_t packed = 0;
+      for (uint64_t i = 0; i < n && !span; ++i) packed += round16(len[i]);
+      if (small_call(n, span ? hi - lo : packed)) {
+        const SmallSpan sp{arena, off, lo, hi};
+        run_small(ctx, t0, n, len, out, [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); },
+                  span ? &sp : nullptr);
+        ctx->stats.direct_calls += span;
+        ctx->stats.messages += n;
+        ctx->stats.message_bytes += sum;
+        ctx->stats.blocks += blocks;
+        return;
+      }
+    }
     // Overlapping payloads (sum of lengths > the span they cover) means there
     // may be aliases: give every message the index of the first message with
     // the same (off, len).
@@ -1572,14 +1707,21 @@ int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
     // Message length of each action = sum of its parts (h.Write appends).
     std::vector<uint64_t>& alen = ctx->tmp_len;
     alen.assign(n_actions, 0);
-    for (uint64_t i = 0; i < n_actions; ++i)
+    uint64_t packed = 0;
+    for (uint64_t i = 0; i < n_actions; ++i) {
       for (uint64_t j = action_part_begin[i]; j < action_part_begin[i + 1]; ++j) alen[i] += part_len[j];
-    run_pipeline(ctx, t0, n_actions, alen.data(), nullptr, out, [&](uint64_t a, uint8_t* dst) {
+      packed += round16(alen[i]);
+    }
+    auto gather = [&](uint64_t a, uint8_t* dst) {
       for (uint64_t j = action_part_begin[a]; j < action_part_begin[a + 1]; ++j) {
         std::memcpy(dst, arena + part_off[j], part_len[j]);
         dst += part_len[j];
       }
-    });
+    };
+    if (small_call(n_actions, packed))
+      run_small(ctx, t0, n_actions, alen.data(), out, gather);
+    else
+      run_pipeline(ctx, t0, n_actions, alen.data(), nullptr, out, gather);
     uint64_t bytes = 0, blocks = 0;
     for (uint64_t i = 0; i < n_actions; ++i) { bytes += alen[i]; blocks += blocks_for(alen[i]); }
     ctx->stats.messages += n_actions;
@@ -1604,7 +1746,22 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
   return guarded(ctx, [&] {
     std::vector<uint64_t>& alen = ctx->tmp_len;
     alen.resize(n);
-    for (uint64_t i = 0; i < n; ++i) alen[i] = 32 * (begin[i + 1] - begin[i]);
+    uint64_t packed = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      alen[i] = 32 * (begin[i + 1] - begin[i]);
+      packed += alen[i];  // multiples of 32: already 16-aligned
+    }
+    if (small_call(n, packed)) {  // the latency path: each Batch's digests packed as one message
+      run_small(ctx, now_ms(), n, alen.data(), out, [&](uint64_t i, uint8_t* dst) {
+        for (uint64_t k = begin[i]; k < begin[i + 1]; ++k, dst += 32) std::memcpy(dst, table + 32 * (uint64_t)idx[k], 32);
+      });
+      uint64_t blocks = 0;
+      for (uint64_t i = 0; i < n; ++i) blocks += blocks_for(alen[i]);
+      ctx->stats.messages += n;
+      ctx->stats.message_bytes += 32 * n_idx;
+      ctx->stats.blocks += blocks;
+      return;
+    }
     const uint32_t k = (uint32_t)ctx->devs.size();
     std::vector<uint64_t> bounds(k + 1);
     partition(alen.data(), n, k, bounds.data());

@@ -29,7 +29,7 @@ def test_exports_via_nm():
 
 
 def test_abi_version():
-    assert L.lib().msha_abi_version() == L.ABI_VERSION == 3
+    assert L.lib().msha_abi_version() == L.ABI_VERSION == 4
 
 
 def test_library_is_gfx950_code_object():
@@ -148,7 +148,7 @@ def test_stats_and_shard_stats_null_args():
     assert lib.msha_shard_count(None, ctypes.byref(n)) == L.MSHA_ERR_INVALID_ARG
     assert lib.msha_get_shard_stats(None, 0, None) == L.MSHA_ERR_INVALID_ARG
     assert ctypes.sizeof(L.MshaShardStats) == 8 * 11
-    assert ctypes.sizeof(L.MshaStats) == 8 * 17
+    assert ctypes.sizeof(L.MshaStats) == 8 * 18
 
 
 def _first_ref(off, ln):

@@ -29,15 +29,31 @@ def _arena_from(msgs, align=16):
     return arena, np.array(offs, dtype=np.uint64), np.array([len(m) for m in msgs], dtype=np.uint64)
 
 
+@pytest.fixture(params=["small", "pipeline"])
+def host_path(request, engine, monkeypatch):
+    """Run a host-API test through the small-call path (one H2D, one launch, one
+    D2H) and through the pipelined path (forced by MSHA_SMALL_BYTES=0), and check
+    which one ran (msha_stats.small_calls)."""
+    if request.param == "pipeline":
+        monkeypatch.setenv("MSHA_SMALL_BYTES", "0")
+    else:
+        monkeypatch.delenv("MSHA_SMALL_BYTES", raising=False)
+        monkeypatch.delenv("MSHA_SMALL_MSGS", raising=False)
+    before = engine.stats()["small_calls"]
+    yield request.param
+    ran = engine.stats()["small_calls"] - before
+    assert ran > 0 if request.param == "small" else ran == 0
+
+
 # ---------------------------------------------------------------- fixtures --
-def test_kat(engine, kat):
+def test_kat(engine, kat, host_path):
     msgs = [v["msg_ascii"].encode() for v in kat["vectors"]] + [b"a" * 1_000_000]
     exp = [v["sha256"] for v in kat["vectors"]] + [kat["million_a"]["sha256"]]
     got = engine.hash_actions([[m] for m in msgs])
     assert [g.hex() for g in got] == exp
 
 
-def test_lengths_golden_one_batch(engine, lengths_golden):
+def test_lengths_golden_one_batch(engine, lengths_golden, host_path):
     msgs = [m for m, _ in lengths_golden]
     arena, off, ln = _arena_from(msgs)
     got = engine.digest_batch(arena, off, ln)
@@ -45,7 +61,7 @@ def test_lengths_golden_one_batch(engine, lengths_golden):
         assert got[i].tobytes() == d, f"len {len(m)}"
 
 
-def test_lengths_golden_unaligned_host_arena(engine, lengths_golden):
+def test_lengths_golden_unaligned_host_arena(engine, lengths_golden, host_path):
     # caller arena with arbitrary (unaligned) offsets: the library repacks
     msgs = [m for m, _ in lengths_golden]
     arena, off, ln = _arena_from(msgs, align=0)
@@ -53,13 +69,13 @@ def test_lengths_golden_unaligned_host_arena(engine, lengths_golden):
     assert [g.tobytes() for g in got] == [d for _, d in lengths_golden]
 
 
-def test_actions_golden(engine, actions_golden):
+def test_actions_golden(engine, actions_golden, host_path):
     got = engine.hash_actions([parts for _, _, parts, _ in actions_golden])
     for (name, _, _, d), g in zip(actions_golden, got):
         assert g == d, name
 
 
-def test_each_length_alone(engine, lengths_golden):
+def test_each_length_alone(engine, lengths_golden, host_path):
     # one-message batches: exercises the launch path at n=1 for every padding case
     for m, d in lengths_golden[:130]:
         assert engine.hash_actions([[m]])[0] == d, len(m)
@@ -671,3 +687,66 @@ def test_concurrent_contexts_on_threads(monkeypatch, shards):
         t.join(timeout=120)
     assert not errs, errs
     assert set(got) == {"a", "b"}
+
+
+# ------------------------------------------------------- small-call path --
+def test_small_path_pinned_span_aliases_and_edges(engine):
+    """The latency path on a pinned, 16-B aligned arena whose span is over 512 KiB
+    (metadata H2D + the caller's span as is): aliases, empty messages, a message
+    ending at the arena's last byte."""
+    rng = np.random.default_rng(7)
+    lens = [0, 1, 55, 56, 63, 64, 119, 120, 512, 600_000, 0]
+    msgs = [rng.integers(0, 256, n, dtype=np.uint8).tobytes() for n in lens]
+    arena, off, ln = _arena_from(msgs)
+    arena = arena[:int(off[-2] + ln[-2])]           # the 600,000-B message ends the arena
+    off = np.concatenate([off[:-1], off[[3, 3, 8]]]).astype(np.uint64)   # aliases of 56 and 512 B
+    ln = np.concatenate([ln[:-1], ln[[3, 3, 8]]]).astype(np.uint64)
+    pinned = engine.pinned_empty(arena.size)
+    pinned[:] = arena
+    st0 = engine.stats()
+    got = engine.digest_batch(pinned, off, ln)
+    st1 = engine.stats()
+    assert st1["small_calls"] == st0["small_calls"] + 1 and st1["direct_calls"] == st0["direct_calls"] + 1
+    exp = [hashlib.sha256(arena[int(o):int(o) + int(n)].tobytes()).digest() for o, n in zip(off, ln)]
+    assert [g.tobytes() for g in got] == exp
+    assert engine.shard_stats()[0]["messages"] == off.size
+    # a small pinned span is packed instead (one H2D): not a direct call
+    st0 = engine.stats()
+    got = engine.digest_batch(pinned, off[:9], ln[:9])
+    st1 = engine.stats()
+    assert st1["small_calls"] == st0["small_calls"] + 1 and st1["direct_calls"] == st0["direct_calls"]
+    assert [g.tobytes() for g in got] == exp[:9]
+
+
+def test_small_path_digest_of_digests_and_actions(engine):
+    """digest-of-digests and hash_actions calls of a few Batches through the latency
+    path: zero-part Batches (SHA256("")), repeated indices, odd and even counts."""
+    rng = np.random.default_rng(11)
+    table = rng.integers(0, 256, size=(64, 32), dtype=np.uint8)
+    counts = [0, 1, 2, 3, 20, 21, 0, 40]
+    begin = np.concatenate([[0], np.cumsum(counts)]).astype(np.uint64)
+    idx = rng.integers(0, 64, size=int(begin[-1]), dtype=np.uint32)
+    st0 = engine.stats()
+    got = engine.digest_of_digests(table, idx, begin)
+    assert engine.stats()["small_calls"] == st0["small_calls"] + 1
+    assert np.array_equal(got, oracle.digest_of_digests(table, idx, begin))
+    actions = [[table[k].tobytes() for k in idx[begin[i]:begin[i + 1]]] for i in range(len(counts))]
+    assert engine.hash_actions(actions) == [bytes(g) for g in got]
+    assert engine.stats()["small_calls"] == st0["small_calls"] + 2
+
+
+def test_small_path_limits(engine, monkeypatch):
+    """A call above MSHA_SMALL_MSGS messages or MSHA_SMALL_BYTES of payload takes the
+    pipelined path; at the limit it takes the small one."""
+    monkeypatch.setenv("MSHA_SMALL_MSGS", "100")
+    monkeypatch.setenv("MSHA_SMALL_BYTES", str(100 * 512))
+    w = W.c2_requests(101)
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    for n, small in ((100, True), (101, False)):
+        st0 = engine.stats()["small_calls"]
+        assert np.array_equal(engine.digest_batch(w.arena, w.off[:n], w.len[:n]), exp[:n])
+        assert engine.stats()["small_calls"] == st0 + int(small), n
+    monkeypatch.setenv("MSHA_SMALL_BYTES", str(100 * 512 - 16))
+    st0 = engine.stats()["small_calls"]
+    assert np.array_equal(engine.digest_batch(w.arena, w.off[:100], w.len[:100]), exp[:100])
+    assert engine.stats()["small_calls"] == st0
