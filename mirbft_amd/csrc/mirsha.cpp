@@ -1007,22 +1007,29 @@ void rerun_unsplit(msha_ctx* ctx, Device& d, const Plan& P, uint8_t* d2h_dst) {
 // actions. run_pipeline's round trip costs ~60-80 us whatever the size (seven
 // queue operations over two streams, events, planning passes), while the GPU
 // floor of H2D + kernel + D2H is ~18 us (tools/op_latency.hip). A call of at
-// most small_msgs() messages and small_bytes() of payload therefore runs on the
-// context's first GPU as: messages packed behind their metadata in one pinned
+// most small_msgs() messages and small_bytes() of payload (limits below)
+// therefore runs on the context's first GPU as: messages packed behind their metadata in one pinned
 // staging buffer -> ONE H2D (a pinned, 16-byte aligned arena span over 512 KiB
 // is uploaded as is instead: metadata H2D + span H2D), one launch, ONE D2H of
 // [error word | digests]. No alias folding (an identical payload is simply hashed again)
-// and no sharding: neither pays at this size. MSHA_SMALL_BYTES (default 1 MiB,
-// 0 disables) and MSHA_SMALL_MSGS (default 4096) set the limits.
+// and no sharding: neither pays at this size.
 // ---------------------------------------------------------------------------
 uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* e = getenv(name);
   return e ? strtoull(e, nullptr, 10) : dflt;
 }
-// read per call (a getenv is ~0.1 us): tests switch paths within one process
-uint64_t small_bytes() { return env_u64("MSHA_SMALL_BYTES", 1ull << 20); }
-uint64_t small_msgs() { return env_u64("MSHA_SMALL_MSGS", 4096); }
-constexpr uint64_t kSmallSpanMin = 512ull << 10;
+// Limits, read per call (a getenv is ~0.1 us; tests switch paths within one
+// process). Measured per call (tools/latency.cpp, profiles/r02_latency/): packing
+// on the calling thread beats the pipeline up to a few MiB (512-B requests: 4,096
+// 132 vs 193 us, 16,384 388 vs 448 us; 65,536 = 32 MiB 2.5 vs 1.3 ms); a pinned
+// span needs no packing and wins up to one 64 MiB upload piece (65,536 x 512 B 861
+// vs 898 us); digest-of-digests keeps its own path above 1 MiB (its table goes up
+// once, nothing is gathered: 4,096 Batches 137 us vs 184 packed).
+uint64_t small_bytes() { return env_u64("MSHA_SMALL_BYTES", 4ull << 20); }   // packed payload; 0 disables
+uint64_t small_msgs() { return env_u64("MSHA_SMALL_MSGS", 65536); }
+uint64_t small_span_bytes() { return std::min<uint64_t>(env_u64("MSHA_SMALL_SPAN_BYTES", kDirectChunk), kDirectChunk); }
+constexpr uint64_t kSmallSpanMin = 512ull << 10;  // below: pack it anyway (one H2D beats two)
+constexpr uint64_t kSmallDodBytes = 1ull << 20;
 inline bool small_call(uint64_t n, uint64_t bytes) {
   return n <= small_msgs() && bytes <= small_bytes() && small_bytes() > 0;
 }
@@ -1647,11 +1654,11 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
       // A pinned arena goes up as is only above 512 KiB: below that, packing it
       // behind the metadata (one H2D instead of two) is the faster of the two
       // (tools/latency.cpp: 32 KiB pinned 57 us as two copies, 44 us packed).
-      const bool span = aligned16 && hi - lo > kSmallSpanMin && hi - lo <= small_bytes() &&
-                        is_pinned_host(arena + lo);
+      const bool span = small_bytes() > 0 && aligned16 && hi - lo > kSmallSpanMin &&
+                        hi - lo <= small_span_bytes() && is_pinned_host(arena + lo);
       uint64_t packed = 0;
       for (uint64_t i = 0; i < n && !span; ++i) packed += round16(len[i]);
-      if (small_call(n, span ? hi - lo : packed)) {
+      if (span || small_call(n, packed)) {
         const SmallSpan sp{arena, off, lo, hi};
         run_small(ctx, t0, n, len, out, [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); },
                   span ? &sp : nullptr);
@@ -1751,7 +1758,7 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
       alen[i] = 32 * (begin[i + 1] - begin[i]);
       packed += alen[i];  // multiples of 32: already 16-aligned
     }
-    if (small_call(n, packed)) {  // the latency path: each Batch's digests packed as one message
+    if (small_call(n, packed) && packed <= kSmallDodBytes) {  // latency path: a Batch's digests = one message
       run_small(ctx, now_ms(), n, alen.data(), out, [&](uint64_t i, uint8_t* dst) {
         for (uint64_t k = begin[i]; k < begin[i + 1]; ++k, dst += 32) std::memcpy(dst, table + 32 * (uint64_t)idx[k], 32);
       });

@@ -107,7 +107,8 @@ int main() {
     for (size_t i = 0; i < reqs.size() && i < r.value.size(); ++i)
       EXPECT(r.value[i] == oracle({reqs[i]}), "request digest == oracle");
   }
-  {  // It("packs the list into a pinned, 16-byte aligned arena that libmirsha uploads as is")
+  {  // It("packs the list into a pinned, 16-byte aligned arena: a short list takes the
+     //     latency path (packed, one H2D), a longer one is uploaded as is")
     msha_stats before{}, after{};
     msha_get_stats(hasher.ctx(), &before);
     ActionList al;
@@ -115,9 +116,19 @@ int main() {
     auto r = processor::ProcessHashActions(hasher, al);
     EXPECT(r.ok(), "no error");
     msha_get_stats(hasher.ctx(), &after);
-    EXPECT(after.direct_calls == before.direct_calls + 1, "direct (zero-copy) upload");
+    EXPECT(after.small_calls == before.small_calls + 1 && after.direct_calls == before.direct_calls,
+           "short list: latency path, packed");
     for (int i = 0; i < 300; ++i)
       EXPECT(r.value.Items()[i].digest == oracle({Bytes(i % 97, (uint8_t)i), Bytes(i % 13, 7)}), "digest");
+    ActionList big;  // ~1.3 MB of payload: over the 512 KiB a pinned arena is packed below
+    for (int i = 0; i < 3000; ++i) big.Hash({Bytes(400 + i % 50, (uint8_t)i), Bytes(i % 13, 9)}, nullptr);
+    before = after;
+    auto r2 = processor::ProcessHashActions(hasher, big);
+    EXPECT(r2.ok(), "no error");
+    msha_get_stats(hasher.ctx(), &after);
+    EXPECT(after.direct_calls == before.direct_calls + 1, "longer list: direct (zero-copy) upload");
+    for (int i = 0; i < 3000; i += 7)
+      EXPECT(r2.value.Items()[i].digest == oracle({Bytes(400 + i % 50, (uint8_t)i), Bytes(i % 13, 9)}), "digest");
   }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);

@@ -73,6 +73,7 @@ def test_split_stall_host_api_reruns_unsplit(engine, monkeypatch, pinned):
         arena = engine.pinned_empty(w.arena.size)
         arena[:] = w.arena
     monkeypatch.setenv("MSHA_SPLIT_STALL", "1")
+    monkeypatch.setenv("MSHA_SMALL_BYTES", "0")      # the pipelined path (the one that splits)
     st0 = engine.stats()
     t0 = time.perf_counter()
     got = engine.digest_batch(arena, w.off, w.len)
@@ -92,6 +93,7 @@ def test_split_stall_digest_of_digests_host_reruns(engine, monkeypatch):
     idx = rng.integers(0, 4096, int(begin[-1]), dtype=np.uint32)
     exp = oracle.digest_of_digests(table, idx, begin)
     monkeypatch.setenv("MSHA_SPLIT_STALL", "1")
+    monkeypatch.setenv("MSHA_SMALL_BYTES", "0")
     st0 = engine.stats()
     assert np.array_equal(engine.digest_of_digests(table, idx, begin), exp)
     st1 = engine.stats()
