@@ -1008,11 +1008,11 @@ void rerun_unsplit(msha_ctx* ctx, Device& d, const Plan& P, uint8_t* d2h_dst) {
 // queue operations over two streams, events, planning passes), while the GPU
 // floor of H2D + kernel + D2H is ~18 us (tools/op_latency.hip). A call of at
 // most small_msgs() messages and small_bytes() of payload (limits below)
-// therefore runs on the context's first GPU as: messages packed behind their metadata in one pinned
-// staging buffer -> ONE H2D (a pinned, 16-byte aligned arena span over 512 KiB
-// is uploaded as is instead: metadata H2D + span H2D), one launch, ONE D2H of
-// [error word | digests]. No alias folding (an identical payload is simply hashed again)
-// and no sharding: neither pays at this size.
+// therefore runs on the context's first GPU as: messages packed behind their
+// metadata in one pinned staging buffer -> ONE H2D (a pinned, 16-byte aligned
+// arena span over 512 KiB is uploaded as is instead: metadata H2D + span H2D),
+// one launch, ONE D2H of [error word | digests]. No alias folding (an identical
+// payload is simply hashed again) and no sharding: neither pays at this size.
 // ---------------------------------------------------------------------------
 uint64_t env_u64(const char* name, uint64_t dflt) {
   const char* e = getenv(name);
