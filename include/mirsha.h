@@ -26,10 +26,12 @@
  *    retains them. Digests are written to caller memory (32 bytes each, in input
  *    order), so the caller can hand out fresh copies (the state machine keeps
  *    digests as map keys: batch_tracker.go:85-91, epoch_change.go:42-50).
- *  - A context is used by one thread at a time (the reference hashes on one
- *    goroutine, mirbft.go:470); distinct contexts may be used concurrently.
- *    Each call selects its device(s) explicitly, so OS-thread migration between
- *    calls (goroutines) is harmless.
+ *  - A context may be shared between threads: calls on one context are
+ *    serialised inside the library (a second caller waits for the first; the
+ *    reference hashes on one goroutine anyway, mirbft.go:470), and distinct
+ *    contexts run concurrently. msha_last_error(ctx) is the context's last
+ *    failure, whichever thread made it. Each call selects its device(s)
+ *    explicitly, so OS-thread migration between calls (goroutines) is harmless.
  *  - There is no CPU fallback: with no usable GPU, msha_ctx_create fails with
  *    MSHA_ERR_NO_DEVICE.
  */

@@ -520,8 +520,11 @@ void plan_direct_lanes(Plan& P, const Device& d, const uint64_t* off, const uint
 }  // namespace
 
 struct msha_ctx {
+  // Calls on one context are serialised here (a second caller waits), so a
+  // context may be shared between threads; distinct contexts run concurrently.
+  mutable std::mutex mu;
   std::vector<Device> devs;
-  std::string err;
+  char err[512] = "";  // last failure on the context (fixed buffer: msha_last_error's pointer stays valid)
   msha_stats stats{};
   std::vector<void*> pinned;  // allocations handed out by msha_pinned_alloc
   std::vector<uint64_t> tmp_len;
@@ -536,7 +539,7 @@ struct msha_ctx {
 namespace {
 
 int fail(msha_ctx* ctx, int code, const std::string& msg) {
-  if (ctx) ctx->err = msg;
+  if (ctx) std::snprintf(ctx->err, sizeof(ctx->err), "%s", msg.c_str());
   return code;
 }
 
@@ -544,7 +547,7 @@ template <class F>
 int guarded(msha_ctx* ctx, F&& f) {
   try {
     f();
-    if (ctx) ctx->err.clear();
+    if (ctx) ctx->err[0] = '\0';
     return MSHA_OK;
   } catch (const MshaError& e) {
     return fail(ctx, e.code, e.what());
@@ -1530,7 +1533,7 @@ int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint
     }
   });
   if (rc != MSHA_OK) {
-    set_create_error(ctx->err, errbuf, errbuf_len);
+    set_create_error(std::string(ctx->err), errbuf, errbuf_len);
     for (auto& d : ctx->devs) d.release();
     delete ctx;
     return rc;
@@ -1554,10 +1557,11 @@ void msha_ctx_destroy(msha_ctx* ctx) {
   delete ctx;
 }
 
-const char* msha_last_error(const msha_ctx* ctx) { return ctx ? ctx->err.c_str() : g_create_error; }
+const char* msha_last_error(const msha_ctx* ctx) { return ctx ? ctx->err : g_create_error; }
 
 int msha_get_stats(const msha_ctx* ctx, msha_stats* out) {
   if (!ctx || !out) return MSHA_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   *out = ctx->stats;
   return MSHA_OK;
 }
@@ -1570,6 +1574,7 @@ int msha_shard_count(const msha_ctx* ctx, uint32_t* n) {
 
 int msha_get_shard_stats(const msha_ctx* ctx, uint32_t shard, msha_shard_stats* out) {
   if (!ctx || !out || shard >= ctx->devs.size()) return MSHA_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
   *out = ctx->devs[shard].st;
   return MSHA_OK;
 }
@@ -1612,6 +1617,8 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
                       const uint64_t* len, uint64_t n, uint8_t* out) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n == 0) return MSHA_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   if (!off || !len || !out || (arena_len && !arena))
     return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   if (n >= 0xffffffffull) return fail(ctx, MSHA_ERR_INVALID_ARG, "more than 2^32-2 messages in one call");
@@ -1699,6 +1706,8 @@ int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
                       const uint64_t* action_part_begin, uint64_t n_actions, uint8_t* out) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n_actions == 0) return MSHA_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   if (!action_part_begin || !out || (n_parts && (!part_off || !part_len)) || (arena_len && !arena))
     return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   if (action_part_begin[0] != 0 || action_part_begin[n_actions] != n_parts)
@@ -1742,6 +1751,8 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
                            uint8_t* out) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n == 0) return MSHA_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   if (!begin || !out || (n_idx && !idx) || (n_table && !table))
     return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   if (begin[0] != 0 || begin[n] != n_idx)
@@ -1864,6 +1875,8 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
                              uint8_t* d_out, void* stream) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n == 0) return MSHA_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   if (!d_arena || !d_off || !d_len || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   return guarded(ctx, [&] {
     hipStream_t st;
@@ -1882,6 +1895,8 @@ int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t s
                                uint64_t msg_len, uint64_t n, uint8_t* d_out, void* stream) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n == 0) return MSHA_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   if (!d_arena || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   if (stride % MSHA_DEVICE_ALIGN) return fail(ctx, MSHA_ERR_ALIGNMENT, "stride must be a multiple of 16");
   return guarded(ctx, [&] {
@@ -1899,6 +1914,8 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
                                   const uint64_t* d_begin, uint64_t n, uint8_t* d_out, void* stream) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   if (n == 0) return MSHA_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   if (!d_table || !d_idx || !d_begin || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   return guarded(ctx, [&] {
     hipStream_t st;
@@ -1914,6 +1931,8 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
 
 int msha_set_kernel_policy(msha_ctx* ctx, int policy) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   if (policy != MSHA_KERNEL_AUTO && policy != MSHA_KERNEL_LANE && policy != MSHA_KERNEL_COOP)
     return fail(ctx, MSHA_ERR_INVALID_ARG, "unknown kernel policy " + std::to_string(policy));
   ctx->kernel_policy = policy;
@@ -1922,6 +1941,8 @@ int msha_set_kernel_policy(msha_ctx* ctx, int policy) {
 
 int msha_device_status(msha_ctx* ctx) {
   if (!ctx || ctx->devs.empty()) return MSHA_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   uint32_t flag = 0;
   int rc = guarded(ctx, [&] {
     Device& d = ctx->devs[0];
@@ -1939,6 +1960,8 @@ int msha_device_status(msha_ctx* ctx) {
 
 int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p) {
   if (!ctx || !p) return MSHA_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   return guarded(ctx, [&] {
     HIPCHK(hipSetDevice(ctx->devs[0].id));
     HIPCHK(hipHostMalloc(p, std::max<uint64_t>(bytes, 1), hipHostMallocPortable));
@@ -1948,6 +1971,8 @@ int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p) {
 
 int msha_pinned_free(msha_ctx* ctx, void* p) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
   auto it = std::find(ctx->pinned.begin(), ctx->pinned.end(), p);
   if (it == ctx->pinned.end()) return fail(ctx, MSHA_ERR_INVALID_ARG, "pointer not from msha_pinned_alloc");
   ctx->pinned.erase(it);

@@ -689,6 +689,47 @@ def test_concurrent_contexts_on_threads(monkeypatch, shards):
     assert set(got) == {"a", "b"}
 
 
+def test_shared_context_on_threads(engine):
+    """mirsha.h: calls on one context are serialised inside the library, so four
+    threads may share it: small and pipelined calls of all three host entry points
+    interleave on one context, every digest right (before the context mutex, the
+    planning buffers of two concurrent calls would have been shared)."""
+    import threading
+    rng = np.random.default_rng(5)
+    wa = W.c5_storm(1 << 15)
+    wb = W.c2_requests(3000)
+    table = rng.integers(0, 256, size=(256, 32), dtype=np.uint8)
+    begin = np.arange(0, 20 * 501, 20, dtype=np.uint64)
+    idx = rng.integers(0, 256, int(begin[-1]), dtype=np.uint32)
+    actions = [[rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in rng.integers(0, 200, 3)]
+               for _ in range(400)]
+    exp = {"a": _oracle_dedup(wa), "b": oracle.digest_batch(wb.arena, wb.off, wb.len),
+           "d": oracle.digest_of_digests(table, idx, begin),
+           "h": [hashlib.sha256(b"".join(p)).digest() for p in actions]}
+    calls = {"a": lambda: engine.digest_batch(wa.arena, wa.off, wa.len),      # pipelined (aliases)
+             "b": lambda: engine.digest_batch(wb.arena, wb.off, wb.len),      # small
+             "d": lambda: engine.digest_of_digests(table, idx, begin),        # small, packed Batches
+             "h": lambda: engine.hash_actions(actions)}                       # small, parts
+    errs = []
+
+    def run(tag):
+        try:
+            for _ in range(8):
+                g = calls[tag]()
+                ok = g == exp[tag] if tag == "h" else np.array_equal(g, exp[tag])
+                if not ok:
+                    errs.append(tag)
+        except Exception as ex:  # surfaced below
+            errs.append(repr(ex))
+
+    th = [threading.Thread(target=run, args=(t,)) for t in calls]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=120)
+    assert not errs, errs
+
+
 # ------------------------------------------------------- small-call path --
 def test_small_path_pinned_span_aliases_and_edges(engine):
     """The latency path on a pinned, 16-B aligned arena whose span is over 512 KiB
