@@ -400,6 +400,11 @@ struct Plan {
   uint64_t lanes = 0;               // messages that get a lane (one per distinct payload)
   std::vector<uint32_t> rep;        // shard-local message -> its lane's message (empty: identity)
   std::vector<uint64_t> cut_chunk;  // direct mode: span chunk lane group g waits for
+  // ordered direct mode: later_min[g] = the lowest message any lane of groups
+  // >= g writes (later_min[groups] = m), so once groups < g are hashed the
+  // digest slots below later_min[g] are final; d2h_done = slots already D2H'd
+  std::vector<uint64_t> later_min;
+  uint64_t d2h_done = 0;
   bool identity() const { return !ordered && rep.empty(); }  // lane q hashes message q
 };
 
@@ -1141,6 +1146,8 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     P.m = 0;
     P.next = 0;
     P.launched = 0;
+    P.d2h_done = 0;
+    P.later_min.clear();
     msha_shard_stats& st = ctx->devs[s].st;
     const uint64_t payload = direct ? st.h2d_payload_bytes : 0;  // queued by upload_direct_spans
     st = msha_shard_stats{};
@@ -1241,6 +1248,22 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (direct) {  // the shard's byte ranges of the caller's pinned arena, uploaded as is
       plan_direct_lanes(P, d, direct->off + d.lo, L, h_off, h_len, d.tmp_dev);
       acc = d.arena_bytes;
+      if (P.ordered) {
+        // Lane groups follow the arena, so a batch laid out in index order
+        // (c5) finishes its digest slots roughly front to back: the lowest
+        // slot each group writes, suffix-minimised, says which prefix of
+        // `out` is final after each launch (streamed back in issue_chunk).
+        const size_t G = P.lane_cut.size() - 1;
+        P.later_min.assign(G + 1, P.m);
+        parallel_chunks(G, plan_threads(P.lanes), [&](unsigned, uint64_t a, uint64_t b) {
+          for (uint64_t g = a; g < b; ++g) {
+            uint64_t mn = P.m;
+            for (uint64_t q = P.lane_cut[g]; q < P.lane_cut[g + 1]; ++q) mn = std::min<uint64_t>(mn, P.perm[q]);
+            P.later_min[g] = mn;
+          }
+        });
+        for (size_t g = G; g-- > 0;) P.later_min[g] = std::min(P.later_min[g], P.later_min[g + 1]);
+      }
     } else {
       // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
       // (lane q's payload lands at h_off[q]; payloads are placed in lane order)
@@ -1374,6 +1397,17 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * l0,
                             d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost, d.stream));
       d.st.d2h_bytes += 32 * lanes;
+    } else if (!P.later_min.empty()) {
+      // Ordered direct lanes: slots below every later group's lowest slot are
+      // final (aliases among them are filled on the host after the sync).
+      const uint64_t x = P.later_min[c + 1];
+      if (x > P.d2h_done) {
+        HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * P.d2h_done,
+                              d.out.as<uint8_t>() + 32 * P.d2h_done, 32 * (x - P.d2h_done),
+                              hipMemcpyDeviceToHost, d.stream));
+        d.st.d2h_bytes += 32 * (x - P.d2h_done);
+        P.d2h_done = x;
+      }
     }
     return !last;
   };
@@ -1399,12 +1433,13 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (m == 0) continue;
     HIPCHK(hipSetDevice(d.id));
     HIPCHK(hipEventRecord(d.ev1, d.stream));
-    if (!plans[s].identity()) {
+    const uint64_t done = plans[s].d2h_done;  // slots streamed back after earlier launches
+    if (!plans[s].identity() && done < m) {
       // d.out is message-ordered (lane q wrote slot perm[q]); a pinned result
       // buffer takes it as is, the aliases' slots are filled on the host below
-      HIPCHK(hipMemcpyAsync(out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>(), d.out.p, 32 * m,
-                            hipMemcpyDeviceToHost, d.stream));
-      d.st.d2h_bytes += 32 * m;
+      HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * done,
+                            d.out.as<uint8_t>() + 32 * done, 32 * (m - done), hipMemcpyDeviceToHost, d.stream));
+      d.st.d2h_bytes += 32 * (m - done);
     }
     HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
     d.st.d2h_bytes += 4;
