@@ -116,7 +116,13 @@ struct PinBuf {
 class WorkerPool {
  public:
   static WorkerPool& get() {
-    static WorkerPool pool(std::min(16u, std::max(1u, std::thread::hardware_concurrency())) - 1);
+    // 16 threads (one GPU's host share), or MSHA_HOST_THREADS; never above the machine's
+    static WorkerPool pool([] {
+      const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+      const char* env = getenv("MSHA_HOST_THREADS");
+      const unsigned want = env ? (unsigned)std::max(1L, std::strtol(env, nullptr, 10)) : 16u;
+      return std::min(want, hw) - 1;
+    }());
     return pool;
   }
   explicit WorkerPool(unsigned helpers) {
@@ -605,7 +611,18 @@ void for_each_shard(msha_ctx* ctx, F&& f) {
     f(0u);
     return;
   }
-  const unsigned per = std::max(1u, std::min(16u, std::max(1u, std::thread::hardware_concurrency())) / k);
+  // Host threads for the whole call: 16 per physical GPU (virtual shards of one
+  // GPU share its 16), at most the machine's, MSHA_HOST_THREADS overriding. On an
+  // 8-GPU node each shard then plans its 1/8 of the batch on 16 threads, as one
+  // GPU plans a whole batch, so planning stays under each link's shorter upload.
+  std::vector<int> ids;
+  for (const Device& d : ctx->devs)
+    if (std::find(ids.begin(), ids.end(), d.id) == ids.end()) ids.push_back(d.id);
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const char* env = getenv("MSHA_HOST_THREADS");
+  const unsigned total = env ? (unsigned)std::max(1L, std::strtol(env, nullptr, 10))
+                             : std::min<unsigned>(hw, 16u * (unsigned)ids.size());
+  const unsigned per = std::max(1u, total / k);
   for (Device& d : ctx->devs)
     if (!d.gather_pool || d.gather_pool->size() != per) d.gather_pool.reset(new WorkerPool(per - 1));
   std::vector<std::exception_ptr> errs(k);
