@@ -16,7 +16,8 @@ prints ONE JSON line. With --config c2 on one GPU the line also carries
 extra_configs (c3 and c4 timed the same way, each with its own roofline
 fraction and verified sample). --mode lib instead times the north-star host
 path in ONE process: one libmirsha context over N GPUs (device_mask), a pinned
-arena, msha_digest_batch per step (PCIe-inclusive; never the headline value). Warmup: the W steps, then more untimed
+arena, msha_digest_batch per step (PCIe-inclusive; never the headline value); the
+default run reports it as host_api (c5 over all N GPUs, a child process). Warmup: the W steps, then more untimed
 steps until --min-warmup-ms (300) of wall time has passed -- MI355X clocks need
 ~100 ms of load to settle, and a cold timed region measures the clock ramp
 (c2: 0.395 ms per launch after 3 warmup steps, 0.330 ms after 200); the line
@@ -89,6 +90,8 @@ def parse():
                         "msha_digest_batch on a pinned arena (end-to-end, PCIe-inclusive)")
     p.add_argument("--pageable", action="store_true", help="with --mode lib: a pageable numpy arena")
     p.add_argument("--no-extra", action="store_true", help="skip the extra_configs (c3, c4) legs")
+    p.add_argument("--no-host-api", action="store_true",
+                   help="skip the host_api leg (c5 through msha_digest_batch over all N GPUs, one process)")
     return p.parse_args()
 
 
@@ -221,6 +224,41 @@ def launch_ranks(args) -> int:
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     return subprocess.run(cmd).returncode
+
+
+def host_api_leg(args, world: int) -> dict:
+    """The north-star host path over the job's N GPUs, reported beside the
+    headline: ONE process, one libmirsha context over device_mask (1 << N) - 1,
+    c5's 2^23 mixed actions (strong scaling: the node's storm split over its
+    GPUs by cumulative blocks) from a pinned arena through msha_digest_batch,
+    digests straight back into pinned memory (bench.py --mode lib). Run as a
+    child process after the ranks have released their GPUs, so a failure there
+    costs this object, never the headline line."""
+    import subprocess
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK",
+                        "ROLE_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    gpus = world
+    if args.share_device:       # ranks on one GPU: its virtual shards stand in for the GPUs
+        env["MSHA_VIRTUAL_SHARDS"] = str(world)
+        gpus = 1
+    cmd = [sys.executable, os.path.abspath(__file__), "--mode", "lib", "--config", "c5", "--gpus", str(gpus),
+           "--steps", "5", "--warmup", "2"]
+    try:
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+        lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not lines:
+            return {"error": f"rc={r.returncode}", "stderr_tail": r.stderr[-400:]}
+        d = json.loads(lines[-1])
+    except Exception as e:  # noqa: BLE001 -- reported, never fatal to the headline
+        return {"error": repr(e)[:400]}
+    return {"what": "c5 2^23 mixed actions, pinned arena -> msha_digest_batch -> pinned digests, one process, "
+                    "one context over all the job's GPUs (PCIe-inclusive; NOT the headline)",
+            "value": d["value"], "unit": "digests/s", "n_gpus": d["n_gpus"], "shards": d["shards"],
+            "virtual_shards": d["virtual_shards"], "ms_per_call": d["ms_per_step"],
+            "gbps_hashed": d["gbps_hashed"], "steps": d["steps"], "plan_ms": d["last_call_stats"]["plan_ms"],
+            "per_gpu": [{"device": x["device"], "messages": x["messages"], "h2d_bytes": x["h2d_bytes"],
+                         "device_ms": x["device_ms"]} for x in d["last_call_shards"]]}
 
 
 def kind_of(st0: dict, st1: dict) -> str:
@@ -496,10 +534,14 @@ def main():
             line["extra_configs"] = {c: extra_config(eng, c, args, dev, stream) for c in ("c3", "c4")}
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
-        print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
+        dist.barrier()              # every rank has released its GPU
         dist.destroy_process_group()
+    if rank == 0:
+        if not args.no_host_api:
+            line["host_api"] = host_api_leg(args, world)
+        print(json.dumps(line), flush=True)
 
 
 if __name__ == "__main__":
