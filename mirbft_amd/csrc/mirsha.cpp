@@ -528,6 +528,26 @@ void plan_direct_lanes(Plan& P, const Device& d, const uint64_t* off, const uint
   }
 }
 
+// Ordered direct lanes: lane groups follow the arena, so a batch laid out in
+// index order (c5) finishes its digest slots roughly front to back. The lowest
+// slot each group writes, suffix-minimised (later_min[g] = min over lanes of
+// groups >= g, later_min[groups] = m), says which prefix of the digest slots is
+// final once groups < g are hashed; issue_chunk streams it back per launch.
+void plan_stream_back(Plan& P) {
+  const size_t G = P.lane_cut.size() - 1;
+  P.later_min.assign(G + 1, P.m);
+  parallel_chunks(G, std::min<unsigned>(plan_threads(P.lanes), (unsigned)std::max<size_t>(G, 1)),
+                  [&](unsigned, uint64_t a, uint64_t b) {
+                    for (uint64_t g = a; g < b; ++g) {
+                      uint64_t mn = P.m;
+                      for (uint64_t q = P.lane_cut[g]; q < P.lane_cut[g + 1]; ++q)
+                        mn = std::min<uint64_t>(mn, P.perm[q]);
+                      P.later_min[g] = mn;
+                    }
+                  });
+  for (size_t g = G; g-- > 0;) P.later_min[g] = std::min(P.later_min[g], P.later_min[g + 1]);
+}
+
 }  // namespace
 
 struct msha_ctx {
@@ -1265,22 +1285,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     if (direct) {  // the shard's byte ranges of the caller's pinned arena, uploaded as is
       plan_direct_lanes(P, d, direct->off + d.lo, L, h_off, h_len, d.tmp_dev);
       acc = d.arena_bytes;
-      if (P.ordered) {
-        // Lane groups follow the arena, so a batch laid out in index order
-        // (c5) finishes its digest slots roughly front to back: the lowest
-        // slot each group writes, suffix-minimised, says which prefix of
-        // `out` is final after each launch (streamed back in issue_chunk).
-        const size_t G = P.lane_cut.size() - 1;
-        P.later_min.assign(G + 1, P.m);
-        parallel_chunks(G, plan_threads(P.lanes), [&](unsigned, uint64_t a, uint64_t b) {
-          for (uint64_t g = a; g < b; ++g) {
-            uint64_t mn = P.m;
-            for (uint64_t q = P.lane_cut[g]; q < P.lane_cut[g + 1]; ++q) mn = std::min<uint64_t>(mn, P.perm[q]);
-            P.later_min[g] = mn;
-          }
-        });
-        for (size_t g = G; g-- > 0;) P.later_min[g] = std::min(P.later_min[g], P.later_min[g + 1]);
-      }
+      if (P.ordered) plan_stream_back(P);
     } else {
       // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
       // (lane q's payload lands at h_off[q]; payloads are placed in lane order)

@@ -185,6 +185,18 @@ static void direct_lane_cases(std::mt19937_64& rng) {
         CHECK(chunk(q) == P.cut_chunk[g], "direct shape %d: lane %llu outside its group's chunk", shape,
               (unsigned long long)q);
     CHECK(shape != 0 || !P.ordered, "a uniform ascending request batch keeps identity lanes");
+    if (P.ordered) {  // streamed D2H: later_min[g] = lowest slot written by groups >= g
+      plan_stream_back(P);
+      const size_t G = P.lane_cut.size() - 1;
+      bool ok = P.later_min.size() == G + 1 && P.later_min[G] == m;
+      uint64_t mn = m;
+      for (size_t g = G; g-- > 0 && ok;) {
+        for (uint64_t q = P.lane_cut[g]; q < P.lane_cut[g + 1]; ++q) mn = std::min<uint64_t>(mn, P.perm[q]);
+        ok &= P.later_min[g] == mn;
+      }
+      CHECK(ok, "direct shape %d: later_min is not the suffix minimum of the groups' slots", shape);
+      CHECK(shape != 2 || P.later_min[1] == 0, "reversed lanes: nothing is final before the last group");
+    }
   }
 }
 

@@ -18,3 +18,16 @@ def test_host_planning_under_asan_ubsan():
                        timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     assert "all checks passed" in r.stdout
+
+
+def test_host_planning_under_tsan():
+    """The same harness under ThreadSanitizer: the planning phases run on the
+    worker pool at these sizes (>= 2^18 items), so a race between its threads is
+    reported (the reference's CI runs ginkgo --race)."""
+    subprocess.run(["make", "-s", "-C", CPP, "tsan"], check=True, timeout=600)
+    env = dict(os.environ, TSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(CPP, "build", "host_planning_tsan")], capture_output=True, text=True,
+                       timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "all checks passed" in r.stdout
+    assert "WARNING: ThreadSanitizer" not in r.stderr
