@@ -1,7 +1,8 @@
 // Host-only timing of the planning steps of msha_digest_batch on a c5-shaped
 // batch (8M messages: 70% 512 B, 25% k x 32 B, 5% aliases of 100 ~49 KB
 // payloads). No GPU: the helpers are compiled straight from mirsha.cpp.
-// Build: hipcc -O3 -std=c++17 -o tools/plan_bench tools/plan_bench.cpp -lpthread
+// Build: g++ -O3 -std=c++17 -D__HIP_PLATFORM_AMD__ -I/opt/rocm/include -Wno-subobject-linkage \
+//        -o tools/plan_bench tools/plan_bench.cpp -L/opt/rocm/lib -lamdhip64 -Wl,-rpath,/opt/rocm/lib -pthread
 #include "../mirbft_amd/csrc/mirsha.cpp"
 
 #include <cstdio>
@@ -10,16 +11,18 @@
 
 // The launchers live in kernels.hip; this host-only harness never launches.
 namespace msha {
+bool plan_split(uint64_t, int, int, SplitPlan*) { return false; }
 hipError_t launch_digest_batch(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*,
-                               const uint32_t*, uint64_t, uint8_t*, uint32_t*, int, int, hipStream_t) {
-  return hipErrorNotSupported;
-}
-hipError_t launch_digest_of_digests(const uint8_t*, const uint32_t*, const uint64_t*, uint64_t, uint8_t*,
-                                    hipStream_t) {
+                               const uint32_t*, uint64_t, uint8_t*, uint32_t*, int, int, hipStream_t,
+                               const SplitPlan*, LaunchKind*) {
   return hipErrorNotSupported;
 }
 hipError_t launch_digest_uniform(const uint8_t*, uint64_t, uint64_t, uint64_t, uint8_t*, uint32_t*, int,
-                                 hipStream_t) {
+                                 hipStream_t, LaunchKind*) {
+  return hipErrorNotSupported;
+}
+hipError_t launch_digest_of_digests(const uint8_t*, const uint32_t*, const uint64_t*, uint64_t, uint8_t*,
+                                    uint32_t*, hipStream_t, const SplitPlan*, LaunchKind*) {
   return hipErrorNotSupported;
 }
 }  // namespace msha
