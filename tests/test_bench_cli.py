@@ -51,3 +51,30 @@ def test_verify_sample_hits_every_lane_position():
     bad[65535, 0] ^= 1                              # the last digest is always sampled
     with pytest.raises(SystemExit):
         bench.verify_sample(w, bad)
+
+
+def test_host_api_leg_failure_is_reported_not_fatal(monkeypatch):
+    """The host_api leg runs `bench.py --mode lib` as a child after the headline
+    is timed; when the child fails (here: no GPU, so no context) the leg returns
+    an error object instead of raising, so the headline line is still printed.
+    The torchrun variables are not passed on (the child is one process over all
+    the job's GPUs), and --share-device maps the ranks onto virtual shards."""
+    sys.path.insert(0, ROOT)
+    import bench
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--share-device"])
+    args = bench.parse()
+    seen = {}
+    real_run = subprocess.run
+
+    def spy(cmd, *a, **k):
+        seen["cmd"], seen["env"] = cmd, k.get("env", {})
+        return real_run(cmd + ["--no-host-api"], *a, **k)
+
+    monkeypatch.setenv("WORLD_SIZE", "2")
+    monkeypatch.setenv("MASTER_PORT", "29999")
+    monkeypatch.setattr(subprocess, "run", spy)
+    res = bench.host_api_leg(args, 2)
+    assert "error" in res, res
+    assert seen["cmd"][2:] == ["--mode", "lib", "--config", "c5", "--gpus", "1", "--steps", "5", "--warmup", "2"]
+    assert "WORLD_SIZE" not in seen["env"] and "MASTER_PORT" not in seen["env"]
+    assert seen["env"]["MSHA_VIRTUAL_SHARDS"] == "2"
