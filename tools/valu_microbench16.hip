@@ -1,0 +1,123 @@
+// Integer-VALU microbenchmark, part 16 (gfx950): per-opcode issue class. Part
+// 15: a wave of `v_alignbit` (H) and a wave of `v_add` (F) on one SIMD overlap,
+// yet a realistic message-schedule F stream (shifts by constants, v_bitop3, an
+// add with a literal) paired with itself runs at ~4 cycles per instruction, so
+// one of those forms is not in the fast class. For every form below: two waves
+// of it on one SIMD (X+X: ~2.3 cycles per instruction for the fast class, ~4.3
+// for the slow one) and one wave of it beside one wave of v_alignbit (H+X: the
+// fast class overlaps, ~2.5).
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/valu_microbench16 tools/valu_microbench16.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+#define CHECK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
+  fprintf(stderr, "HIP error %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
+
+constexpr int ITERS = 4096;
+#define CLOB "v32","v33","v34","v35","v36","v37","v38","v39","v40","v41","v42","v43","v44","v45","v46","v47", \
+             "v48","v49","v50","v51","v52","v53","v54","v55","vcc","s4","s5"
+// 8 independent instances of a form: OP(d, a, b)
+#define R8(M) M(48, 32, 33) M(49, 34, 35) M(50, 36, 37) M(51, 38, 39) M(52, 40, 41) M(53, 42, 43) M(54, 44, 45) M(55, 46, 47)
+#define O_ALIGN(d, a, b) "v_alignbit_b32 v" #d ", v" #a ", v" #a ", 7\n"
+#define O_ADD(d, a, b) "v_add_u32_e32 v" #d ", v" #a ", v" #b "\n"
+#define O_ADDLIT(d, a, b) "v_add_u32_e32 v" #d ", 0x428a2f98, v" #a "\n"
+#define O_ADDINL(d, a, b) "v_add_u32_e32 v" #d ", 5, v" #a "\n"
+#define O_SUB(d, a, b) "v_sub_u32_e32 v" #d ", v" #a ", v" #b "\n"
+#define O_SHRC(d, a, b) "v_lshrrev_b32_e32 v" #d ", 7, v" #a "\n"
+#define O_SHRV(d, a, b) "v_lshrrev_b32_e32 v" #d ", v47, v" #a "\n"
+#define O_SHLC(d, a, b) "v_lshlrev_b32_e32 v" #d ", 25, v" #a "\n"
+#define O_SHRC64(d, a, b) "v_lshrrev_b32_e64 v" #d ", 7, v" #a "\n"
+#define O_XOR(d, a, b) "v_xor_b32_e32 v" #d ", v" #a ", v" #b "\n"
+#define O_OR(d, a, b) "v_or_b32_e32 v" #d ", v" #a ", v" #b "\n"
+#define O_AND(d, a, b) "v_and_b32_e32 v" #d ", v" #a ", v" #b "\n"
+#define O_MOV(d, a, b) "v_mov_b32_e32 v" #d ", v" #a "\n"
+#define O_BOP96(d, a, b) "v_bitop3_b32 v" #d ", v" #a ", v" #b ", v46 bitop3:0x96\n"
+#define O_BOPCA(d, a, b) "v_bitop3_b32 v" #d ", v" #a ", v" #b ", v46 bitop3:0xca\n"
+#define O_BOPE8(d, a, b) "v_bitop3_b32 v" #d ", v" #a ", v" #b ", v46 bitop3:0xe8\n"
+#define O_XAD(d, a, b) "v_xad_u32 v" #d ", v" #a ", v" #b ", v46\n"
+#define O_BFI(d, a, b) "v_bfi_b32 v" #d ", v" #a ", v" #b ", v46\n"
+#define O_ADD3(d, a, b) "v_add3_u32 v" #d ", v" #a ", v" #b ", v46\n"
+#define O_ADD3S(d, a, b) "v_add3_u32 v" #d ", v" #a ", v" #b ", s4\n"
+#define O_PERM(d, a, b) "v_perm_b32 v" #d ", v" #a ", v" #a ", s5\n"
+#define O_LSHLOR(d, a, b) "v_lshl_or_b32 v" #d ", v" #a ", 25, v" #b "\n"
+#define O_ANDOR(d, a, b) "v_and_or_b32 v" #d ", v" #a ", v" #b ", v46\n"
+#define O_OR3(d, a, b) "v_or3_b32 v" #d ", v" #a ", v" #b ", v46\n"
+#define O_ADDCO(d, a, b) "v_add_co_u32_e32 v" #d ", vcc, v" #a ", v" #b "\n"
+#define O_PKADD16(d, a, b) "v_pk_add_u16 v" #d ", v" #a ", v" #b "\n"
+#define O_ADDSGPR(d, a, b) "v_add_u32_e32 v" #d ", s4, v" #a "\n"
+#define O_BOPS(d, a, b) "v_bitop3_b32 v" #d ", v" #a ", v" #b ", s4 bitop3:0x96\n"
+#define O_LSHLADD(d, a, b) "v_lshl_add_u32 v" #d ", v" #a ", 3, v" #b "\n"
+#define O_ADD64(d, a, b) "v_lshl_add_u64 v[48:49], v[32:33], 0, v[34:35]\n"
+
+#define FORMS(X) X(ALIGN) X(ADD) X(ADDLIT) X(ADDINL) X(SUB) X(SHRC) X(SHRV) X(SHLC) X(SHRC64) X(XOR) X(OR) \
+  X(AND) X(MOV) X(BOP96) X(BOPCA) X(BOPE8) X(XAD) X(BFI) X(ADD3) X(ADD3S) X(PERM) X(LSHLOR) X(ANDOR) X(OR3) \
+  X(ADDCO) X(PKADD16) X(ADDSGPR) X(BOPS) X(LSHLADD)
+#define ENUM(N) k##N,
+enum { FORMS(ENUM) kCount };
+#define NAME(N) #N,
+static const char* kNames[] = {FORMS(NAME)};
+
+template <int K>
+__device__ __forceinline__ void run() {
+#define CASE(N) if (K == k##N) { for (int i = 0; i < ITERS; ++i) asm volatile(R8(O_##N) R8(O_##N) R8(O_##N) R8(O_##N) ::: CLOB); }
+  FORMS(CASE)
+#undef CASE
+}
+
+template <int K0, int K1>
+__global__ __launch_bounds__(512) void k_pair(unsigned* out, unsigned seed) {
+  const int kind = (threadIdx.x >> 6) < 4 ? K0 : K1;
+  unsigned x = seed ^ threadIdx.x;
+  asm volatile("v_mov_b32 v32, %0\n v_mov_b32 v33, %0\n v_mov_b32 v34, %0\n v_mov_b32 v35, %0\n"
+               "v_mov_b32 v36, %0\n v_mov_b32 v37, %0\n v_mov_b32 v38, %0\n v_mov_b32 v39, %0\n"
+               "v_mov_b32 v40, %0\n v_mov_b32 v41, %0\n v_mov_b32 v42, %0\n v_mov_b32 v43, %0\n"
+               "v_mov_b32 v44, %0\n v_mov_b32 v45, %0\n v_mov_b32 v46, %0\n v_mov_b32 v47, 13\n"
+               "s_mov_b32 s4, 0x71374491\n s_mov_b32 s5, 0x00010203\n" :: "v"(x) : CLOB);
+  if (kind == K0) run<K0>(); else run<K1>();
+  unsigned y;
+  asm volatile("v_xor_b32 %0, v48, v49" : "=v"(y));
+  out[blockIdx.x * blockDim.x + threadIdx.x] = y;
+}
+
+int main() {
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, 0));
+  const int cus = p.multiProcessorCount;
+  unsigned* out;
+  CHECK(hipMalloc(&out, sizeof(unsigned) * cus * 512));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+  struct Case { int a, b; void (*f)(unsigned*, unsigned); };
+#define PAIRS(N) Case{k##N, k##N, k_pair<k##N, k##N>}, Case{kALIGN, k##N, k_pair<kALIGN, k##N>},
+  const Case cs[] = {FORMS(PAIRS)};
+  {
+    hipEvent_t w0, w1;
+    CHECK(hipEventCreate(&w0)); CHECK(hipEventCreate(&w1));
+    CHECK(hipEventRecord(w0));
+    for (float el = 0; el < 500.f;) {
+      for (int i = 0; i < 8; ++i) hipLaunchKernelGGL((k_pair<kALIGN, kALIGN>), dim3(cus * 4), dim3(512), 0, 0, out, 1u);
+      CHECK(hipEventRecord(w1));
+      CHECK(hipEventSynchronize(w1));
+      CHECK(hipEventElapsedTime(&el, w0, w1));
+    }
+  }
+  for (const Case& c : cs) {
+    hipLaunchKernelGGL(c.f, dim3(cus), dim3(512), 0, 0, out, 1u);
+    CHECK(hipDeviceSynchronize());
+    float best = 1e30f;
+    for (int r = 0; r < 5; ++r) {
+      CHECK(hipEventRecord(e0));
+      hipLaunchKernelGGL(c.f, dim3(cus), dim3(512), 0, 0, out, 3u + r);
+      CHECK(hipEventRecord(e1));
+      CHECK(hipEventSynchronize(e1));
+      float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+      best = ms < best ? ms : best;
+    }
+    const double instr = (double)ITERS * 32 * 2;  // per SIMD (two waves)
+    printf("{\"pair\": \"%s+%s\", \"ms\": %.4f, \"simd_cycles_per_instr_at_2.4GHz\": %.3f}\n", kNames[c.a], kNames[c.b],
+           best, best * 1e-3 * 2.4e9 / instr);
+    fflush(stdout);
+  }
+  return 0;
+}
