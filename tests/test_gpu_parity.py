@@ -478,6 +478,31 @@ def test_pinned_direct_chunked_span(engine, layout, pinned_out):
     assert np.array_equal(got, exp)
 
 
+@pytest.mark.parametrize("pinned_out", [False, True])
+def test_pinned_direct_streamed_digests_shuffled(engine, pinned_out):
+    """Ordered direct lanes stream their digests back after each launch (the
+    slots below the lowest slot any later lane group writes). A c5 batch whose
+    messages are shuffled within index windows -- slot order and arena order
+    agree only roughly, so each launch finalises a different, ragged prefix --
+    plus aliases, over several 64 MiB upload pieces: every digest bit-exact."""
+    w = W.c5_storm(1 << 19)
+    rng = np.random.default_rng(5)
+    perm = np.arange(w.n)
+    for a in range(0, w.n, 4096):          # shuffle inside 4,096-message windows
+        rng.shuffle(perm[a:a + 4096])
+    w.off = w.off[perm].copy()
+    w.len = w.len[perm].copy()
+    exp = _oracle_dedup(w)
+    pinned = engine.pinned_empty(w.arena.size)
+    pinned[:] = w.arena
+    out = engine.pinned_empty(w.n * 32).reshape(w.n, 32) if pinned_out else None
+    before = engine.stats()["direct_calls"]
+    got = engine.digest_batch(pinned, w.off, w.len, out=out)
+    assert engine.stats()["direct_calls"] == before + 1
+    assert np.array_equal(got, exp)
+    assert w.arena.size > 3 * (64 << 20)   # several upload pieces, several lane groups
+
+
 def test_pinned_direct_chunked_sharded(monkeypatch):
     """The chunked direct path over 2 virtual shards of one GPU (each shard its own span)."""
     from mirbft_amd import Engine
