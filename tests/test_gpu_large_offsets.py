@@ -107,3 +107,33 @@ def test_digest_of_digests_table_beyond_4gib(engine):
     assert np.array_equal(out.cpu().numpy(), exp)
     del table
     torch.cuda.empty_cache()
+
+
+def test_message_bit_length_above_32_bits(engine):
+    """FIPS 180-4 appends the message length in bits as a 64-bit big-endian word;
+    at 2^29 bytes (512 MiB) the bit length passes 2^32 and its high 32-bit word
+    becomes nonzero. One wave of messages over one shared 512 MiB payload, with
+    lengths just under, at and past 2^29 bytes across every padding case (tail
+    r = 0, 1, 55, 56, 63, 64 + ..., one-block and two-block padding), hashed
+    through the host entry point with the cooperative and the lane kernels.
+    Expected digests: hashlib over the common prefix once, then each tail."""
+    base = 1 << 29
+    lens = [base - 1, base, base + 1, base + 55, base + 56, base + 63, base + 64, base + 119, base + 120]
+    rng = np.random.default_rng(29)
+    arena = rng.integers(0, 256, base + 256, dtype=np.uint8)
+    pre = hashlib.sha256(memoryview(arena[:base - 1]))
+    exp = []
+    for n in lens:
+        h = pre.copy()
+        h.update(memoryview(arena[base - 1:n]))
+        exp.append(np.frombuffer(h.digest(), dtype=np.uint8))
+    exp = np.stack(exp)
+    off = np.zeros(len(lens), dtype=np.uint64)
+    ln = np.array(lens, dtype=np.uint64)
+    for policy in ("coop", "lane"):
+        engine.set_kernel_policy(policy)
+        try:
+            got = engine.digest_batch(arena, off, ln)
+        finally:
+            engine.set_kernel_policy("auto")
+        assert np.array_equal(got, exp), policy
