@@ -565,6 +565,10 @@ struct msha_ctx {
   std::vector<uint64_t> uid;
   std::vector<uint64_t> alias_table, alias_bucket;
   std::vector<uint32_t> alias_tag;
+  // Several physical GPUs: the whole-batch planning phases (validation, alias
+  // detection, upload marking) run on a pool of the context's full host-thread
+  // share (host_threads_total) instead of the process-wide 16; made on first use.
+  std::unique_ptr<WorkerPool> wide;
 };
 
 namespace {
@@ -574,9 +578,35 @@ int fail(msha_ctx* ctx, int code, const std::string& msg) {
   return code;
 }
 
+// Host threads for a call on ctx: 16 per physical GPU (virtual shards of one
+// GPU share its 16), at most the machine's, MSHA_HOST_THREADS overriding. On an
+// 8-GPU node each shard then plans its 1/8 of the batch on 16 threads, as one
+// GPU plans a whole batch, so planning stays under each link's shorter upload.
+unsigned host_threads_total(const msha_ctx* ctx) {
+  std::vector<int> ids;
+  for (const Device& d : ctx->devs)
+    if (std::find(ids.begin(), ids.end(), d.id) == ids.end()) ids.push_back(d.id);
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const char* env = getenv("MSHA_HOST_THREADS");
+  return env ? (unsigned)std::max(1L, std::strtol(env, nullptr, 10))
+             : std::min<unsigned>(hw, 16u * (unsigned)std::max<size_t>(ids.size(), 1));
+}
+
 template <class F>
 int guarded(msha_ctx* ctx, F&& f) {
+  struct PoolScope {  // the context's wide pool for this call's whole-batch phases
+    WorkerPool* prev = tl_pool;
+    explicit PoolScope(msha_ctx* c) {
+      if (c && !c->devs.empty()) {
+        const unsigned total = host_threads_total(c);
+        if (!c->wide && total > WorkerPool::get().size()) c->wide.reset(new WorkerPool(total - 1));
+        if (c->wide) tl_pool = c->wide.get();
+      }
+    }
+    ~PoolScope() { tl_pool = prev; }
+  };
   try {
+    PoolScope scope(ctx);
     f();
     if (ctx) ctx->err[0] = '\0';
     return MSHA_OK;
@@ -631,18 +661,7 @@ void for_each_shard(msha_ctx* ctx, F&& f) {
     f(0u);
     return;
   }
-  // Host threads for the whole call: 16 per physical GPU (virtual shards of one
-  // GPU share its 16), at most the machine's, MSHA_HOST_THREADS overriding. On an
-  // 8-GPU node each shard then plans its 1/8 of the batch on 16 threads, as one
-  // GPU plans a whole batch, so planning stays under each link's shorter upload.
-  std::vector<int> ids;
-  for (const Device& d : ctx->devs)
-    if (std::find(ids.begin(), ids.end(), d.id) == ids.end()) ids.push_back(d.id);
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const char* env = getenv("MSHA_HOST_THREADS");
-  const unsigned total = env ? (unsigned)std::max(1L, std::strtol(env, nullptr, 10))
-                             : std::min<unsigned>(hw, 16u * (unsigned)ids.size());
-  const unsigned per = std::max(1u, total / k);
+  const unsigned per = std::max(1u, host_threads_total(ctx) / k);
   for (Device& d : ctx->devs)
     if (!d.gather_pool || d.gather_pool->size() != per) d.gather_pool.reset(new WorkerPool(per - 1));
   std::vector<std::exception_ptr> errs(k);

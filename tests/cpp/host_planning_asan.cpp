@@ -200,9 +200,35 @@ static void direct_lane_cases(std::mt19937_64& rng) {
   }
 }
 
+// A context over several physical GPUs runs its whole-batch phases on a pool of
+// its full host-thread share (guarded() installs it for the call, then restores
+// the caller's pool); alias detection on it matches the reference.
+static void wide_pool_case(std::mt19937_64& rng) {
+  setenv("MSHA_HOST_THREADS", "12", 1);
+  {
+    msha_ctx ctx;
+    ctx.devs.resize(2);
+    ctx.devs[0].id = 0;
+    ctx.devs[1].id = 1;  // two physical GPUs: host_threads_total = 12 (the override)
+    unsigned seen = 0;
+    const int rc = guarded(&ctx, [&] { seen = plan_threads(1u << 20); });
+    CHECK(rc == MSHA_OK && seen == 12, "wide pool: %u threads (rc %d)", seen, rc);
+    CHECK(tl_pool == nullptr, "wide pool: caller's pool not restored");
+    const uint64_t n = (1u << 20) + 3;
+    std::vector<uint64_t> off(n), len(n);
+    for (uint64_t i = 0; i < n; ++i) {
+      len[i] = rng() % 300;
+      off[i] = rng() % 16 == 0 ? (rng() % 64) * 512 : (1u << 20) + 512 * i;
+    }
+    guarded(&ctx, [&] { check_alias("wide pool", off, len); });
+  }
+  unsetenv("MSHA_HOST_THREADS");
+}
+
 int main() {
   std::mt19937_64 rng(0x4D49524246540000ull);
   alias_cases(rng);
+  wide_pool_case(rng);
   order_cases(rng);
   partition_cases(rng);
   direct_lane_cases(rng);
