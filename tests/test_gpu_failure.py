@@ -9,6 +9,7 @@ batch_tracker.go:192-195; errors surface through doHashWork, mirbft.go:290-293):
   * host entry points: the shard is re-hashed unsplit in the same call, every
     digest is correct, and msha_stats.split_retries counts it.
 """
+import os
 import time
 
 import numpy as np
@@ -19,7 +20,9 @@ from mirbft_amd import _lib as L
 from mirbft_amd import workloads as W
 from oracle import oracle
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu,
+              pytest.mark.skipif(os.environ.get("MSHA_SPLIT") == "0",
+                                 reason="split chaining disabled (MSHA_SPLIT=0 A/B run): nothing to stall")]
 
 
 def _cus():

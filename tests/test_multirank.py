@@ -86,5 +86,8 @@ def test_bench_two_ranks_on_the_engine():
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["kernel"] == "lane"
+    # c2 runs the lane kernel (a forced MSHA_LOAD_MODE=3 A/B run makes it the pipelined one)
+    want = "pipe" if os.environ.get("MSHA_LOAD_MODE") == "3" else "lane"
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["kernel"] == want
+    assert "error" not in d["host_api"] and d["host_api"]["shards"] == 2
     assert d["value"] > 0 and d["config"]["messages_per_gpu"] == 1 << 20
