@@ -13,7 +13,7 @@ when WORLD_SIZE is unset), every rank hashes its own disjoint 2^20-request
 slice (weak scaling, no collective on the data path); the timed region is
 bracketed by barrier + synchronize and the max over ranks is taken. Rank 0
 prints ONE JSON line. With --config c2 on one GPU the line also carries
-extra_configs (c3 and c4 timed the same way, each with its own roofline
+extra_configs (c3, c4 and c5 timed the same way, each with its own roofline
 fraction and verified sample). --mode lib instead times the north-star host
 path in ONE process: one libmirsha context over N GPUs (device_mask), a pinned
 arena, msha_digest_batch per step (PCIe-inclusive; never the headline value); the
@@ -89,7 +89,7 @@ def parse():
                         "one libmirsha context over N GPUs (device_mask) and the host entry point "
                         "msha_digest_batch on a pinned arena (end-to-end, PCIe-inclusive)")
     p.add_argument("--pageable", action="store_true", help="with --mode lib: a pageable numpy arena")
-    p.add_argument("--no-extra", action="store_true", help="skip the extra_configs (c3, c4) legs")
+    p.add_argument("--no-extra", action="store_true", help="skip the extra_configs (c3, c4, c5) legs")
     p.add_argument("--no-host-api", action="store_true",
                    help="skip the host_api leg (c5 through msha_digest_batch over all N GPUs, one process)")
     return p.parse_args()
@@ -375,7 +375,7 @@ def roofline(w, kern_ms: float, cfg: str) -> dict:
 def extra_config(eng, cfg: str, args, dev, stream) -> dict:
     """One more config timed like the headline (kernel-resident, same warmup and
     K), with its own roofline fraction and a verified sample: puts c3/c4 under
-    the driver's clock next to c2."""
+    the driver's clock next to c2 (c3, c4 and c5 in the default run)."""
     import torch
     w = build_workload(cfg, 0, 1)
     step, d_out = kernel_step(eng, w, cfg, dev, stream)
@@ -531,7 +531,7 @@ def main():
         if world == 1 and args.config == "c2" and not args.no_extra:
             del step, d_out
             torch.cuda.empty_cache()
-            line["extra_configs"] = {c: extra_config(eng, c, args, dev, stream) for c in ("c3", "c4")}
+            line["extra_configs"] = {c: extra_config(eng, c, args, dev, stream) for c in ("c3", "c4", "c5")}
         if not args.no_cpu_baseline and world == 1:
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
     eng.close()
