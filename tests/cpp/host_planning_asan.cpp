@@ -107,7 +107,37 @@ static void order_cases(std::mt19937_64& rng) {
   }
 }
 
+// Plain sequential statement of the partition rule: bounds[s] = the first i
+// whose block-range midpoint acc_i + b_i / 2 reaches total * s / k.
+static std::vector<uint64_t> partition_ref(const std::vector<uint64_t>& len, uint32_t k) {
+  const uint64_t n = len.size();
+  std::vector<uint64_t> b(k + 1, 0);
+  unsigned __int128 total = 0;
+  for (uint64_t l : len) total += blocks_for(l);
+  uint64_t i = 0, acc = 0;
+  for (uint32_t s = 1; s < k; ++s) {
+    while (i < n && (unsigned __int128)2 * k * acc + (unsigned __int128)k * blocks_for(len[i]) < 2 * s * total)
+      acc += blocks_for(len[i++]);
+    b[s] = i;
+  }
+  b[k] = n;
+  return b;
+}
+
 static void partition_cases(std::mt19937_64& rng) {
+  // the threaded partition (chunk sums, one short scan per bound) against the
+  // sequential rule, on batches large enough to run on several threads
+  for (uint64_t n : {(1ull << 18) + 7, (1ull << 20) + 1})
+    for (int shape = 0; shape < 3; ++shape)
+      for (uint32_t k : {2u, 3u, 7u, 8u, 64u}) {
+        std::vector<uint64_t> len(n);
+        for (uint64_t i = 0; i < n; ++i)
+          len[i] = shape == 0 ? 512 : shape == 1 ? rng() % 5000 : (i == n / 3 ? (1ull << 34) : rng() % 100);
+        std::vector<uint64_t> b(k + 1);
+        partition(len.data(), n, k, b.data());
+        CHECK(b == partition_ref(len, k), "partition n=%llu shape=%d k=%u differs from the sequential rule",
+              (unsigned long long)n, shape, k);
+      }
   for (uint64_t n : {0ull, 1ull, 3ull, 100000ull})
     for (uint32_t k : {1u, 2u, 3u, 8u}) {
       std::vector<uint64_t> len(n), b(k + 1);
