@@ -23,7 +23,7 @@ if [[ $STEPS == all || $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == all || $STEPS == *prof* ]]; then
   rm -rf gpurun_out/prof
-  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --config ${PCFG:-c2} --no-cpu-baseline > gpurun_out/prof_bench.log 2>&1; stop_on_fault $? rocprof
+  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --config ${PCFG:-c2} --no-cpu-baseline --no-extra --no-host-api > gpurun_out/prof_bench.log 2>&1; stop_on_fault $? rocprof
   find gpurun_out/prof -name "*kernel_stats*" | head -3
   for f in $(find gpurun_out/prof -name "*kernel_stats.csv"); do cat $f; done
 fi
