@@ -1,8 +1,12 @@
+//go:build mirsha
+// +build mirsha
+
 // Parity of the GPU-batched hash path against the reference's own CPU path
 // (plain `go test`, beside the package's existing suites). Every test skips when
-// libmirsha finds no GPU (MSHA_ERR_NO_DEVICE); run on a box with a GPU:
+// libmirsha finds no GPU (MSHA_ERR_NO_DEVICE). Built with the mirsha tag only;
+// run on a box with a GPU:
 //
-//	go test ./pkg/processor/ -run GPU -v
+//	go test -tags mirsha ./pkg/processor/ -run GPU -v
 package processor
 
 import (
