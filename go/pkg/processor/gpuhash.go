@@ -66,8 +66,8 @@ type GPUHasher struct {
 	ctx    *C.msha_ctx
 	arena  pinnedBuf
 	out    pinnedBuf
-	off    []uint64
-	length []uint64
+	off    pinnedBuf // uint64 per message
+	length pinnedBuf // uint64 per message
 }
 
 type pinnedBuf struct {
@@ -97,7 +97,7 @@ func (g *GPUHasher) Close() {
 	if g.ctx == nil {
 		return
 	}
-	for _, p := range []*pinnedBuf{&g.arena, &g.out} {
+	for _, p := range []*pinnedBuf{&g.arena, &g.out, &g.off, &g.length} {
 		if p.base != nil {
 			C.msha_pinned_free(g.ctx, p.base)
 			p.base, p.buf = nil, nil
@@ -108,9 +108,12 @@ func (g *GPUHasher) Close() {
 }
 
 func (g *GPUHasher) fail(rc C.int) error {
-	// msha_last_error(ctx) is per context, and the context is used under g.mutex
-	// only, so the text belongs to this call whatever thread reads it.
-	return errors.Errorf("libmirsha error %d: %s", int(rc), C.GoString(C.msha_last_error(g.ctx)))
+	// The context is used under g.mutex only, so the text belongs to this call
+	// whatever thread reads it; msha_last_error_copy also reads it under the
+	// library's own lock.
+	var buf [512]C.char
+	C.msha_last_error_copy(g.ctx, &buf[0], C.uint64_t(len(buf)))
+	return errors.Errorf("libmirsha error %d: %s", int(rc), C.GoString(&buf[0]))
 }
 
 // ensure returns p's buffer resized to n bytes (grown in pinned memory on demand).
@@ -133,11 +136,21 @@ func (g *GPUHasher) ensure(p *pinnedBuf, n int) ([]byte, error) {
 	return p.buf, nil
 }
 
+// words returns p's buffer resized to n uint64 values (pinned, grown on demand).
+func (g *GPUHasher) words(p *pinnedBuf, n int) ([]uint64, error) {
+	b, err := g.ensure(p, 8*n)
+	if err != nil {
+		return nil, err
+	}
+	return (*[1 << 37]uint64)(unsafe.Pointer(&b[0]))[:n:n], nil
+}
+
 // digests hashes n messages in one msha_digest_batch call. size bounds the
 // packed arena (every message's bytes plus up to 15 bytes of alignment); pack(i,
 // dst) copies message i's bytes to dst and returns their count. Messages are
-// placed 16-byte aligned, so the library uploads the arena without a staging
-// copy. Returns n fresh 32-byte digests.
+// placed 16-byte aligned and the arena, offsets, lengths and digests all live in
+// pinned memory, so the library DMAs them as they are (no staging copy) and
+// plans the lanes on the GPU. Returns n fresh 32-byte digests.
 func (g *GPUHasher) digests(n int, size int, pack func(i int, dst []byte) int) ([][]byte, error) {
 	g.mutex.Lock()
 	defer g.mutex.Unlock()
@@ -156,11 +169,14 @@ func (g *GPUHasher) digests(n int, size int, pack func(i int, dst []byte) int) (
 	if err != nil {
 		return nil, err
 	}
-	if cap(g.off) < n {
-		g.off = make([]uint64, n)
-		g.length = make([]uint64, n)
+	off, err := g.words(&g.off, n)
+	if err != nil {
+		return nil, err
 	}
-	off, length := g.off[:n], g.length[:n]
+	length, err := g.words(&g.length, n)
+	if err != nil {
+		return nil, err
+	}
 	pos := 0
 	for i := 0; i < n; i++ {
 		off[i] = uint64(pos)

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 4u
+#define MSHA_ABI_VERSION 5u
 
 enum {
   MSHA_OK = 0,
@@ -70,9 +70,11 @@ typedef struct {
   uint64_t message_bytes;  /* sum of unpadded message lengths */
   uint64_t blocks;         /* 64-byte compressions performed */
   /* Last host-memory call, milliseconds of wall time: */
-  double plan_ms;          /* validation, alias detection, sharding, size-class order, placement */
+  double plan_ms;          /* host planning: validation .. every shard's work queued (pinned
+                              arenas: .. the last shard's kernels queued, lanes planned on the GPU) */
   double pack_ms;          /* gathering payload bytes into pinned staging (summed over shards) */
-  double device_ms;        /* first upload .. last kernel on the device (HIP events, max over GPUs) */
+  double device_ms;        /* first upload .. last kernel on the device (HIP events, max over GPUs;
+                              msha_shard_stats splits it into upload_ms and kernel_ms) */
   double total_ms;         /* whole call */
   uint64_t direct_calls;   /* host calls whose arena was uploaded as is (pinned, 16-B aligned) */
   /* Kernel launches by kind, cumulative over every entry point: */
@@ -103,7 +105,13 @@ typedef struct {
   double gather_begin_ms;      /* pageable arenas: first / last gather into pinned staging */
   double gather_end_ms;
   double gather_ms;            /* time spent gathering (sum over chunks) */
-  double device_ms;            /* first upload .. last kernel (HIP events) */
+  double device_ms;            /* first H2D (metadata or payload) starts .. last kernel ends (HIP
+                                  events on the shard's copy and compute streams) */
+  double upload_ms;            /* first H2D starts .. last payload H2D ends: h2d_bytes / upload_ms
+                                  is the shard's achieved PCIe rate */
+  double kernel_ms;            /* first hash kernel starts .. last kernel ends */
+  double first_launch_ms;      /* host: call start .. the shard's first hash kernel enqueued */
+  double plan_kernel_ms;       /* pinned arenas: the GPU lane planner's kernels (plan.hip) */
 } msha_shard_stats;
 
 uint32_t msha_abi_version(void);
@@ -124,7 +132,15 @@ int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint
  * several threads create contexts). */
 int msha_ctx_create(uint32_t device_mask, msha_ctx** out);
 void msha_ctx_destroy(msha_ctx* ctx);
+/* The context's last failure (ctx == NULL: the last failed creation). The
+ * pointer stays valid for the context's life, but another thread's failing call
+ * on the same context may rewrite the text while it is read: read it only while
+ * no other call runs on the context, or use msha_last_error_copy. */
 const char* msha_last_error(const msha_ctx* ctx);
+/* Copy of the same text into buf (NUL-terminated, truncated to buf_len - 1),
+ * taken under the context's lock: safe while other threads use the context.
+ * Returns the text's full length. */
+uint64_t msha_last_error_copy(const msha_ctx* ctx, char* buf, uint64_t buf_len);
 int msha_get_stats(const msha_ctx* ctx, msha_stats* out);
 /* Shards of the context (GPUs in device_mask, or virtual shards). */
 int msha_shard_count(const msha_ctx* ctx, uint32_t* n);

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -70,6 +70,10 @@ class MshaShardStats(ctypes.Structure):
         ("gather_end_ms", ctypes.c_double),
         ("gather_ms", ctypes.c_double),
         ("device_ms", ctypes.c_double),
+        ("upload_ms", ctypes.c_double),
+        ("kernel_ms", ctypes.c_double),
+        ("first_launch_ms", ctypes.c_double),
+        ("plan_kernel_ms", ctypes.c_double),
     ]
 
 
@@ -82,6 +86,7 @@ SIGNATURES = {
                                            ctypes.c_uint64]),
     "msha_ctx_destroy": (None, [_ctxp]),
     "msha_last_error": (ctypes.c_char_p, [_ctxp]),
+    "msha_last_error_copy": (ctypes.c_uint64, [_ctxp, ctypes.c_char_p, ctypes.c_uint64]),
     "msha_get_stats": (ctypes.c_int, [_ctxp, ctypes.POINTER(MshaStats)]),
     "msha_shard_count": (ctypes.c_int, [_ctxp, ctypes.POINTER(ctypes.c_uint32)]),
     "msha_get_shard_stats": (ctypes.c_int, [_ctxp, ctypes.c_uint32, ctypes.POINTER(MshaShardStats)]),

@@ -47,4 +47,37 @@ hipError_t launch_digest_of_digests(const uint8_t* table, const uint32_t* idx,
                                     uint32_t* err, hipStream_t st,
                                     const SplitPlan* split = nullptr, LaunchKind* kind = nullptr);
 
+// Direct (pinned-arena) host calls upload a shard's byte ranges in device-space
+// pieces of 2^kDirectChunkShift bytes (64 MiB), one event each.
+constexpr unsigned kDirectChunkShift = 26;
+
+// Device-side planning of one shard of a direct host call (plan.hip). Every
+// array is device memory of the shard's GPU; m messages, shard-local indices.
+struct PlanArgs {
+  const uint64_t* off;    // caller offsets (raw, as passed to msha_digest_batch)
+  const uint64_t* len;
+  const uint64_t* gmap;   // uploaded granule g (caller offset glo + g << gshift) -> device
+                          // offset, indexed g - gbase
+  uint64_t glo = 0, gbase = 0;
+  uint32_t gshift = 16;
+  uint64_t m = 0;
+  uint64_t* dev_off;      // out: device offset of each message
+  uint32_t* table;        // alias table, tmask + 1 zeroed entries; null: no aliases
+  uint64_t tmask = 0;
+  uint32_t* slot;         // m: each message's table slot (with table)
+  uint32_t* rep;          // out, m: the first message with the same (off, len)
+  uint64_t chunks = 1;    // upload pieces of the shard
+  uint64_t B = 1;         // block-count classes per piece (1: pieces only)
+  uint64_t bmax = 0;      // largest block count (key = piece * B + bmax - blocks)
+  uint64_t nb = 1;        // chunks * B buckets
+  uint32_t* cnt;          // nb zeroed counters -> bucket starts
+  uint32_t* gmin;         // chunks entries, 0xFFFFFFFF-filled: lowest lane index per piece
+  uint32_t* cut;          // out, chunks + 1: first lane of each piece's group
+  uint32_t* info;         // out: [0] = lanes
+  uint64_t* lane_off;     // out, per lane: device offset, length, digest slot
+  uint64_t* lane_len;
+  uint32_t* lane_slot;
+};
+hipError_t launch_plan(const PlanArgs& a, hipStream_t st);
+
 }  // namespace msha

@@ -201,34 +201,33 @@ class WorkerPool {
 // Per-GPU state: stream, timing events, device buffers, pinned staging.
 struct Device {
   int id = 0;
+  uint32_t index = 0;  // shard number in the context
   int cus = 256;
   hipStream_t stream = nullptr;       // kernels (and everything on single-stream paths)
   hipStream_t copy_stream = nullptr;  // H2D of staged chunks, overlapping the kernels
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // device_ms / upload_ms / kernel_ms of the last host call: first H2D (copy
+  // stream) .. last H2D, first hash kernel .. last kernel (msha_shard_stats)
+  hipEvent_t ev_up0 = nullptr, ev_up1 = nullptr, ev_k0 = nullptr;
+  hipEvent_t ev_meta = nullptr, ev_plan = nullptr;  // direct path: metadata landed / GPU plan done
+  hipEvent_t ev_p0 = nullptr, ev_p1 = nullptr;      // direct path: the planner kernels (plan_kernel_ms)
   hipEvent_t slot_free[2] = {nullptr, nullptr};  // staging slot s may be refilled
   hipEvent_t chunk_in = nullptr;                 // last chunk's bytes are on the device
-  std::vector<hipEvent_t> span_ev;               // direct mode: span chunk c is on the device
+  std::vector<hipEvent_t> span_ev;               // direct mode: upload piece c is on the device
   DevBuf arena, off, len, order, out, err, idx, begin, table;
   PinBuf h_arena, h_meta, h_out, slot[2];
   // small-call path (run_small): [meta | payload] in, [error word | digests] out
   DevBuf sm_in, sm_out;
   PinBuf sm_stage, sm_res;
+  // direct path, planned on the GPU (plan.hip): raw metadata, granule map,
+  // device offsets, alias table and slots, representatives, bucket counters,
+  // [gmin | cut | info] read back to h_small; rep read back to h_rep
+  DevBuf p_meta, p_gmap, p_devoff, p_table, p_slot, p_rep, p_cnt, p_small;
+  PinBuf h_gmap, h_small, h_rep;
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
-  // Direct mode: the byte ranges of the caller's arena this shard's messages
-  // touch, at granule resolution (upload_direct_spans): caller offset o lives
-  // at device offset direct_map[(o - direct_glo) >> direct_gshift] + the
-  // offset inside the granule. Untouched granules are neither uploaded nor
-  // given device memory.
-  uint64_t direct_glo = 0;
-  unsigned direct_gshift = 16;
-  std::vector<uint64_t> direct_map;
-  std::vector<uint8_t> direct_mark;
-  uint64_t direct_remap(uint64_t o) const {
-    const uint64_t r = o - direct_glo;
-    return direct_map[r >> direct_gshift] + (r & ((1ull << direct_gshift) - 1));
-  }
+  std::vector<uint8_t> direct_mark;  // direct path: granules of the arena this shard touches
   msha_shard_stats st{};          // last host call (msha_get_shard_stats)
   // Multi-GPU host calls: this GPU's share of the host threads (its shard is
   // planned, and its pageable chunks gathered, on them) and planning scratch.
@@ -241,11 +240,15 @@ struct Device {
   uint64_t split_epoch = 0;
   void release() {
     gather_pool.reset();
-    for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table, &sm_in, &sm_out}) b->release();
+    for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table, &sm_in, &sm_out, &p_meta,
+                      &p_gmap, &p_devoff, &p_table, &p_slot, &p_rep, &p_cnt, &p_small})
+      b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
-    for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1], &sm_stage, &sm_res}) b->release();
-    for (hipEvent_t* e : {&ev0, &ev1, &slot_free[0], &slot_free[1], &chunk_in}) {
+    for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1], &sm_stage, &sm_res, &h_gmap, &h_small, &h_rep})
+      b->release();
+    for (hipEvent_t* e : {&ev0, &ev1, &ev_up0, &ev_up1, &ev_k0, &ev_meta, &ev_plan, &ev_p0, &ev_p1, &slot_free[0],
+                          &slot_free[1], &chunk_in}) {
       if (*e) (void)hipEventDestroy(*e);
       *e = nullptr;
     }
@@ -274,9 +277,16 @@ const msha::SplitPlan* split_for(Device& d, uint64_t n, int policy, msha::SplitP
 }
 
 // MSHA_TRACE=1: host-side phase timestamps (ms since the call began) on stderr.
-inline void trace(const char* what, double t0) {
+inline bool trace_on() {
   static const bool on = getenv("MSHA_TRACE") != nullptr;
-  if (on) fprintf(stderr, "[msha] %-24s %9.2f ms\n", what, now_ms() - t0);
+  return on;
+}
+inline void trace(const char* what, double t0) {
+  if (trace_on()) fprintf(stderr, "[msha] %-24s %9.2f ms\n", what, now_ms() - t0);
+}
+// the same, for one shard's thread of a multi-shard call
+inline void trace(const char* what, uint32_t shard, double t0) {
+  if (trace_on()) fprintf(stderr, "[msha] shard %u %-16s %9.2f ms\n", shard, what, now_ms() - t0);
 }
 
 // Host planning of large batches runs on a few threads: [0, n) is split into
@@ -370,21 +380,13 @@ bool all_equal_blocks(const uint64_t* len, uint64_t n) {
   return true;
 }
 
-void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
-  if (k == 1) {
-    bounds[0] = 0;
-    bounds[1] = n;
-    return;
-  }
-  // bounds[s] = the first message whose block-range midpoint reaches s/k of the
-  // total: acc_i + b_i / 2 >= total * s / k, in integers 2k acc_i + k b_i >=
-  // 2 s total (acc_i = blocks before i). Midpoints never decrease, so each bound
-  // lies in the one 64 K-message piece where the running count crosses the
-  // target: one threaded pass for the piece sums, then one short scan per bound
-  // (a serial pass over c5's 8 M messages cost 30-45 ms before any upload began).
-  constexpr uint64_t kPiece = 1u << 16;  // messages per counted piece: a bound's scan stays short
+// Messages per counted piece of the partition: a bound's scan stays short.
+constexpr uint64_t kPiece = 1u << 16;
+
+// csum[p] = blocks of the messages before piece p (P + 1 entries), threaded.
+void piece_sums(const uint64_t* len, uint64_t n, std::vector<uint64_t>& csum) {
   const uint64_t P = std::max<uint64_t>(1, (n + kPiece - 1) / kPiece);
-  std::vector<uint64_t> csum(P + 1, 0);
+  csum.assign(P + 1, 0);
   parallel_chunks(P, std::min<unsigned>(plan_threads(n), (unsigned)P), [&](unsigned, uint64_t p0, uint64_t p1) {
     for (uint64_t p = p0; p < p1; ++p) {
       uint64_t sum = 0;
@@ -393,6 +395,17 @@ void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
     }
   });
   for (uint64_t p = 0; p < P; ++p) csum[p + 1] += csum[p];
+}
+
+// bounds[s] = the first message whose block-range midpoint reaches s/k of the
+// total: acc_i + b_i / 2 >= total * s / k, in integers 2k acc_i + k b_i >=
+// 2 s total (acc_i = blocks before i). Midpoints never decrease, so each bound
+// lies in the one piece where the running count crosses the target: one short
+// scan per bound over the piece sums (a serial pass over c5's 8 M messages cost
+// 30-45 ms before any upload began).
+void partition_pieces(const uint64_t* len, uint64_t n, uint32_t k, const std::vector<uint64_t>& csum,
+                      uint64_t* bounds) {
+  const uint64_t P = csum.size() - 1;
   using u128 = unsigned __int128;
   const u128 total = csum[P];
   auto bound = [&](uint32_t s) -> uint64_t {
@@ -415,164 +428,43 @@ void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
   bounds[k] = n;
 }
 
-// Direct-mode uploads go out in chunks of this size, each with its own event,
-// so kernels over the lanes whose payloads have landed start while the rest of
-// the span is still crossing PCIe (and their digests come back meanwhile).
-constexpr uint64_t kDirectChunk = 64ull << 20;
+void partition(const uint64_t* len, uint64_t n, uint32_t k, uint64_t* bounds) {
+  if (k == 1) {
+    bounds[0] = 0;
+    bounds[1] = n;
+    return;
+  }
+  std::vector<uint64_t> csum;
+  piece_sums(len, n, csum);
+  partition_pieces(len, n, k, csum, bounds);
+}
+
+// Direct-mode uploads go out in device-space pieces of this size, each with its
+// own event, so kernels over the lanes whose payloads have landed start while
+// the rest is still crossing PCIe (and their digests come back meanwhile).
+constexpr uint64_t kDirectChunk = 1ull << msha::kDirectChunkShift;
 
 // Per-GPU plan of one host-memory call (kept in the context: its vectors are
 // reused call after call, so planning does not page-fault fresh memory).
 struct Plan {
   uint64_t m = 0;
   bool ordered = false;
-  std::vector<uint32_t> perm;       // sorted lane -> shard-local message
-  std::vector<uint64_t> lane_cut;   // chunk boundaries in sorted lanes
-  size_t next = 0;                  // next chunk to issue
+  std::vector<uint32_t> perm;       // sorted lane -> shard-local message (pageable path)
+  std::vector<uint64_t> lane_cut;   // group boundaries in sorted lanes
+  size_t next = 0;                  // next group to issue
   uint64_t launched = 0;            // lanes [0, launched) have a kernel enqueued
   uint64_t lanes = 0;               // messages that get a lane (one per distinct payload)
   std::vector<uint32_t> rep;        // shard-local message -> its lane's message (empty: identity)
-  std::vector<uint64_t> cut_chunk;  // direct mode: span chunk lane group g waits for
-  // ordered direct mode: later_min[g] = the lowest message any lane of groups
-  // >= g writes (later_min[groups] = m), so once groups < g are hashed the
-  // digest slots below later_min[g] are final; d2h_done = slots already D2H'd
+  const uint32_t* rep_dev = nullptr;  // direct path: the same, planned on the GPU (pinned copy)
+  std::vector<uint64_t> cut_chunk;  // direct mode: upload piece lane group g waits for
+  // direct mode: later_min[g] = the lowest message any lane of groups >= g
+  // writes (later_min[groups] = m), so once groups < g are hashed the digest
+  // slots below later_min[g] are final; d2h_done = slots already D2H'd
   std::vector<uint64_t> later_min;
   uint64_t d2h_done = 0;
   bool identity() const { return !ordered && rep.empty(); }  // lane q hashes message q
+  const uint32_t* rep_of() const { return rep_dev ? rep_dev : (rep.empty() ? nullptr : rep.data()); }
 };
-
-
-// Direct mode: order the shard's lanes (one per distinct payload: rep[i] == i,
-// or every message when rep is empty) and fill their lane-indexed device
-// offsets and lengths, in one fused counting sort. Key = (device upload chunk
-// holding the END of the payload, descending block count): lanes are grouped by
-// the 64 MiB chunk (kDirectChunk) whose event says their payload has landed,
-// so each group is hashed as soon as it lands (c5: the ~13 ms kernel runs
-// under the upload instead of after it), and inside a group a wave's lanes
-// have equal block counts. Stable (index order inside a bucket). Two
-// sequential passes over the messages and one scatter; a request batch whose
-// keys already ascend with the index (identity lanes) skips the scatter.
-// Sets perm, lanes (unchanged), ordered, lane_cut and cut_chunk; h_off/h_len
-// are lane-indexed; tdev is scratch (device offset per message).
-void plan_direct_lanes(Plan& P, const Device& d, const uint64_t* off, const uint64_t* len,
-                       uint64_t* h_off, uint64_t* h_len, std::vector<uint64_t>& tdev) {
-  const uint64_t m = P.m;
-  const bool all = P.rep.empty();
-  const uint32_t* rep = P.rep.data();
-  auto lane = [&](uint64_t i) { return all || rep[i] == i; };
-  const uint64_t chunks = std::max<uint64_t>(1, (d.arena_bytes + kDirectChunk - 1) / kDirectChunk);
-  const unsigned T = plan_threads(m);
-  tdev.resize(m);
-  // pass 0: device offsets, the largest block count
-  std::vector<uint64_t> tmax(T, 0);
-  parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
-    uint64_t mx = 0;
-    for (uint64_t i = a; i < b; ++i) {
-      tdev[i] = d.direct_remap(off[i]);
-      if (lane(i)) mx = std::max(mx, blocks_for(len[i]));
-    }
-    tmax[t] = mx;
-  });
-  uint64_t bmax = *std::max_element(tmax.begin(), tmax.end());
-  // bucket = chunk * B + (bmax - blocks); block classes only while the
-  // per-thread histograms stay small (then: by chunk alone)
-  const bool by_blocks = chunks * (bmax + 1) <= (1u << 20);
-  const uint64_t B = by_blocks ? bmax + 1 : 1;
-  const uint64_t nb = chunks * B;
-  auto key = [&](uint64_t i) -> uint64_t {
-    const uint64_t c = std::min<uint64_t>((tdev[i] + std::max<uint64_t>(len[i], 1) - 1) / kDirectChunk, chunks - 1);
-    return c * B + (by_blocks ? bmax - blocks_for(len[i]) : 0);
-  };
-  // pass 1: histograms; are the keys already ascending (identity order)?
-  std::vector<uint64_t> cnt((size_t)T * nb, 0);
-  std::vector<uint64_t> first_key(T, UINT64_MAX), last_key(T, 0);
-  std::vector<uint8_t> mono(T, 1);
-  parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
-    uint64_t* c = cnt.data() + (size_t)t * nb;
-    uint64_t prev = 0;
-    bool first = true, asc = true;
-    for (uint64_t i = a; i < b; ++i) {
-      if (!lane(i)) continue;
-      const uint64_t k = key(i);
-      c[k]++;
-      if (first) {
-        first_key[t] = k;
-        first = false;
-      } else if (k < prev) {
-        asc = false;
-      }
-      prev = k;
-    }
-    last_key[t] = prev;
-    mono[t] = asc;
-  });
-  bool identity = all;
-  for (unsigned t = 0; t < T && identity; ++t) identity = mono[t];
-  for (unsigned t = 1; t < T && identity; ++t)
-    if (first_key[t] != UINT64_MAX && first_key[t] < last_key[t - 1]) identity = false;
-  // group starts by chunk: lanes with bucket < c * B come before chunk c
-  std::vector<uint64_t> chunk_lanes(chunks, 0);
-  for (unsigned t = 0; t < T; ++t)
-    for (uint64_t k = 0; k < nb; ++k) chunk_lanes[k / B] += cnt[(size_t)t * nb + k];
-  if (identity) {
-    parallel_chunks(m, T, [&](unsigned, uint64_t a, uint64_t b) {
-      for (uint64_t i = a; i < b; ++i) {
-        P.perm[i] = (uint32_t)i;
-        h_off[i] = tdev[i];
-        h_len[i] = len[i];
-      }
-    });
-    P.ordered = false;
-  } else {
-    uint64_t run = 0;  // bucket-major, then thread (= index) order: stable
-    for (uint64_t k = 0; k < nb; ++k)
-      for (unsigned t = 0; t < T; ++t) {
-        const uint64_t x = cnt[(size_t)t * nb + k];
-        cnt[(size_t)t * nb + k] = run;
-        run += x;
-      }
-    parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
-      uint64_t* c = cnt.data() + (size_t)t * nb;
-      for (uint64_t i = a; i < b; ++i) {
-        if (!lane(i)) continue;
-        const uint64_t q = c[key(i)]++;
-        P.perm[q] = (uint32_t)i;
-        h_off[q] = tdev[i];
-        h_len[q] = len[i];
-      }
-    });
-    P.ordered = true;
-  }
-  // lane groups: one per chunk that completes at least one payload
-  P.lane_cut.assign(1, 0);
-  P.cut_chunk.clear();
-  uint64_t acc = 0;
-  for (uint64_t c = 0; c < chunks; ++c) {
-    if (!chunk_lanes[c]) continue;
-    acc += chunk_lanes[c];
-    P.lane_cut.push_back(acc);
-    P.cut_chunk.push_back(c);
-  }
-}
-
-// Ordered direct lanes: lane groups follow the arena, so a batch laid out in
-// index order (c5) finishes its digest slots roughly front to back. The lowest
-// slot each group writes, suffix-minimised (later_min[g] = min over lanes of
-// groups >= g, later_min[groups] = m), says which prefix of the digest slots is
-// final once groups < g are hashed; issue_chunk streams it back per launch.
-void plan_stream_back(Plan& P) {
-  const size_t G = P.lane_cut.size() - 1;
-  P.later_min.assign(G + 1, P.m);
-  parallel_chunks(G, std::min<unsigned>(plan_threads(P.lanes), (unsigned)std::max<size_t>(G, 1)),
-                  [&](unsigned, uint64_t a, uint64_t b) {
-                    for (uint64_t g = a; g < b; ++g) {
-                      uint64_t mn = P.m;
-                      for (uint64_t q = P.lane_cut[g]; q < P.lane_cut[g + 1]; ++q)
-                        mn = std::min<uint64_t>(mn, P.perm[q]);
-                      P.later_min[g] = mn;
-                    }
-                  });
-  for (size_t g = G; g-- > 0;) P.later_min[g] = std::min(P.later_min[g], P.later_min[g + 1]);
-}
 
 }  // namespace
 
@@ -614,8 +506,9 @@ unsigned host_threads_total(const msha_ctx* ctx) {
     if (std::find(ids.begin(), ids.end(), d.id) == ids.end()) ids.push_back(d.id);
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const char* env = getenv("MSHA_HOST_THREADS");
-  return env ? (unsigned)std::max(1L, std::strtol(env, nullptr, 10))
-             : std::min<unsigned>(hw, 16u * (unsigned)std::max<size_t>(ids.size(), 1));
+  const unsigned want = env ? (unsigned)std::max(1L, std::strtol(env, nullptr, 10))
+                            : 16u * (unsigned)std::max<size_t>(ids.size(), 1);
+  return std::min(want, hw);
 }
 
 template <class F>
@@ -965,113 +858,6 @@ constexpr uint64_t kChunkBytes = 32ull << 20;
 // e.g. one EpochChange re-hashed N^2 times, epoch_target.go:486-505); their
 // payload is copied and hashed once per GPU.
 // t0: when the entry point was called (plan_ms includes its validation).
-// direct (may be null): the caller's arena is pinned host memory whose message
-// starts are 16-byte aligned (msha_pinned_alloc); upload_direct_spans() has
-// already queued, per GPU, the byte ranges of it that GPU's messages touch
-// (no gather copy), and off indexes the caller's arena.
-struct Direct {
-  const uint8_t* arena;
-  const uint64_t* off;
-};
-
-// Direct mode: queue, per shard, the byte ranges of the caller's pinned arena
-// that its messages touch for DMA (copy stream) BEFORE the lanes are planned,
-// so PCIe runs while the host builds the alias table, lane order and metadata
-// (a large batch's planning takes about as long as its upload: c5 ~40 ms beside
-// ~65 ms of H2D). The ranges are found at granule resolution (>= 64 KiB, at
-// most 2^20 granules per shard): one pass marks the granules each message
-// covers; runs of marked granules are uploaded back to back into the device
-// arena, and untouched granules cost neither PCIe nor HBM. A shard's
-// contiguous slice of a request batch is one run (one span, as before); a
-// shard of an EpochChange storm uploads its own slice plus only the granules
-// of the shared payload pool its aliases reference, not everything between
-// (before: every shard uploaded min(off)..max(off+len), which with the pool at
-// the arena's start meant shard s of k uploaded ~(s+1)/k of the whole arena).
-// Uploads go out in device-space chunks of kDirectChunk, one event each, so
-// lane groups whose payloads have landed can start hashing. bounds: k+1 entries.
-void upload_direct_spans(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off,
-                         const uint64_t* len, const uint8_t* arena, uint64_t* bounds) {
-  const uint32_t k = (uint32_t)ctx->devs.size();
-  partition(len, n, k, bounds);
-  for_each_shard(ctx, [&](uint32_t s) {
-    Device& d = ctx->devs[s];
-    const uint64_t a = bounds[s], b = bounds[s + 1];
-    d.arena_bytes = 0;
-    d.st.h2d_payload_bytes = 0;
-    if (a == b) return;
-    const unsigned T = plan_threads(b - a);
-    std::vector<uint64_t> tlo(T, UINT64_MAX), thi(T, 0);
-    parallel_chunks(b - a, T, [&](unsigned t, uint64_t x, uint64_t y) {
-      uint64_t l = UINT64_MAX, h = 0;  // thread-local: no false sharing on tlo/thi
-      for (uint64_t i = a + x; i < a + y; ++i) {
-        l = std::min(l, off[i]);
-        h = std::max(h, off[i] + std::max<uint64_t>(len[i], 1));
-      }
-      tlo[t] = l;
-      thi[t] = h;
-    });
-    const uint64_t lo = *std::min_element(tlo.begin(), tlo.end());
-    const uint64_t hi = *std::max_element(thi.begin(), thi.end());
-    unsigned gs = 16;
-    while (((hi - (lo & ~((1ull << gs) - 1))) >> gs) >= (1ull << 20)) ++gs;
-    const uint64_t G = 1ull << gs;
-    const uint64_t glo = lo & ~(G - 1);
-    const uint64_t nG = (hi - glo + G - 1) >> gs;
-    d.direct_glo = glo;
-    d.direct_gshift = gs;
-    std::vector<uint8_t>& mark = d.direct_mark;
-    mark.assign(nG, 0);
-    parallel_chunks(b - a, T, [&](unsigned, uint64_t x, uint64_t y) {
-      for (uint64_t i = a + x; i < a + y; ++i) {
-        const uint64_t g0 = (off[i] - glo) >> gs;
-        const uint64_t g1 = (off[i] + std::max<uint64_t>(len[i], 1) - 1 - glo) >> gs;
-        for (uint64_t g = g0; g <= g1; ++g)
-          if (!__atomic_load_n(&mark[g], __ATOMIC_RELAXED)) __atomic_store_n(&mark[g], 1, __ATOMIC_RELAXED);
-      }
-    });
-    d.direct_map.resize(nG);
-    uint64_t dev_bytes = 0;
-    for (uint64_t g = 0; g < nG; ++g) {
-      d.direct_map[g] = mark[g] ? dev_bytes : UINT64_MAX;
-      dev_bytes += mark[g] ? G : 0;
-    }
-    d.arena_bytes = dev_bytes;
-    HIPCHK(hipSetDevice(d.id));
-    d.arena.ensure(d.arena_bytes + msha::kArenaSlack);
-    const uint64_t chunks = std::max<uint64_t>(1, (d.arena_bytes + kDirectChunk - 1) / kDirectChunk);
-    while (d.span_ev.size() < chunks) {
-      hipEvent_t e;
-      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-      d.span_ev.push_back(e);
-    }
-    // runs of marked granules, clipped to [lo, hi), in ascending device order;
-    // event c is recorded once every byte below device offset (c+1)*kDirectChunk is queued
-    uint64_t c = 0, uploaded = 0;
-    for (uint64_t g = 0; g < nG;) {
-      if (!mark[g]) {
-        ++g;
-        continue;
-      }
-      uint64_t g1 = g;
-      while (g1 < nG && mark[g1]) ++g1;
-      const uint64_t h0 = std::max(lo, glo + g * G), h1 = std::min(hi, glo + g1 * G);
-      for (uint64_t pos = h0; pos < h1;) {
-        const uint64_t dev = d.direct_remap(pos);
-        const uint64_t piece = std::min(h1 - pos, (dev / kDirectChunk + 1) * kDirectChunk - dev);
-        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + dev, arena + pos, piece, hipMemcpyHostToDevice,
-                              d.copy_stream));
-        uploaded += piece;
-        pos += piece;
-        for (; c < chunks && (c + 1) * kDirectChunk <= dev + piece; ++c)
-          HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
-      }
-      g = g1;
-    }
-    for (; c < chunks; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
-    d.st.h2d_payload_bytes = uploaded;
-  });
-  trace("direct ranges queued", t0);
-}
 
 // Re-run shard s of a host call in one unsplit launch over all its lanes, after
 // a split-chain handoff timed out (error bit 2: some of its digests are
@@ -1211,12 +997,145 @@ void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_
   ctx->stats.total_ms = now_ms() - t0;
 }
 
+// Launch shard d's lanes accumulated since its last launch, up to the end of
+// lane group c, once they fill the GPU (2 waves per SIMD) or at the last group:
+// hashing runs ~30x faster than PCIe delivers bytes, so a launch per group would
+// only buy overlap worth a few % while a group of large messages (512 x 64 KiB)
+// leaves most SIMDs idle for the whole of its long chains. Then bring back the
+// digests that are final: identity lanes' own slots, or (ordered lanes with
+// later_min) every slot below the lowest slot a later group writes -- into the
+// caller's buffer itself when it is pinned -- while later groups upload.
+void launch_lanes(msha_ctx* ctx, Device& d, Plan& P, size_t c, bool last, double t0, uint8_t* out,
+                  bool out_pinned) {
+  const uint64_t q1 = P.lane_cut[c + 1];
+  const uint64_t fill = (uint64_t)d.cus * 4 * 64 * 2;
+  if (!last && q1 - P.launched < fill) return;
+  const uint64_t l0 = P.launched, lanes = q1 - l0;
+  P.launched = q1;
+  if (l0 == 0) {
+    HIPCHK(hipEventRecord(d.ev_k0, d.stream));
+    d.st.first_launch_ms = now_ms() - t0;
+    trace("first launch", d.index, t0);
+  }
+  // off/len are lane-indexed; out_idx maps lane -> shard-local message
+  // (identity placement: lane q is message q)
+  msha::SplitPlan sp;
+  msha::LaunchKind kind;
+  HIPCHK(msha::launch_digest_batch(
+      d.arena.as<uint8_t>(), d.off.as<uint64_t>() + l0, d.len.as<uint64_t>() + l0, nullptr,
+      P.ordered ? d.order.as<uint32_t>() + l0 : nullptr, lanes,
+      d.out.as<uint8_t>() + (P.ordered ? 0 : 32 * l0), d.err.as<uint32_t>(), d.cus,
+      ctx->kernel_policy, d.stream, split_for(d, lanes, ctx->kernel_policy, sp), &kind));
+  count_launch(ctx, &d, kind);
+  uint8_t* dst = out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>();
+  if (P.identity()) {
+    HIPCHK(hipMemcpyAsync(dst + 32 * l0, d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost,
+                          d.stream));
+    d.st.d2h_bytes += 32 * lanes;
+  } else if (!P.later_min.empty()) {
+    // aliases among the streamed slots are filled on the host after the sync
+    const uint64_t x = P.later_min[c + 1];
+    if (x > P.d2h_done) {
+      HIPCHK(hipMemcpyAsync(dst + 32 * P.d2h_done, d.out.as<uint8_t>() + 32 * P.d2h_done, 32 * (x - P.d2h_done),
+                            hipMemcpyDeviceToHost, d.stream));
+      d.st.d2h_bytes += 32 * (x - P.d2h_done);
+      P.d2h_done = x;
+    }
+  }
+}
+
+// Queue the end of shard d's call on its stream: ev1 after its last kernel,
+// the digest slots not streamed back yet, the error word.
+void queue_tail(Device& d, Plan& P, uint8_t* out, bool out_pinned) {
+  const uint64_t m = P.m;
+  if (m == 0) return;
+  HIPCHK(hipSetDevice(d.id));
+  HIPCHK(hipEventRecord(d.ev1, d.stream));
+  const uint64_t done = P.d2h_done;  // slots streamed back after earlier launches
+  if (!P.identity() && done < m) {
+    // d.out is message-ordered (lane q wrote its message's slot); a pinned result
+    // buffer takes it as is, the aliases' slots are filled on the host afterwards
+    HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * done,
+                          d.out.as<uint8_t>() + 32 * done, 32 * (m - done), hipMemcpyDeviceToHost, d.stream));
+    d.st.d2h_bytes += 32 * (m - done);
+  }
+  HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
+  d.st.d2h_bytes += 4;
+}
+
+float elapsed_ms(hipEvent_t a, hipEvent_t b) {
+  float ms = 0;
+  HIPCHK(hipEventSynchronize(b));
+  HIPCHK(hipEventElapsedTime(&ms, a, b));
+  return ms;
+}
+
+// Wait for every shard of the call, re-run a shard whose split chain timed
+// out, fill the aliases' digests (each copies its representative's) and record
+// the call's figures: device_ms = first upload .. last kernel, upload_ms = first
+// .. last upload, kernel_ms = first kernel .. last kernel (HIP events).
+void join_shards(msha_ctx* ctx, double t0, double t_plan, uint8_t* out, bool out_pinned) {
+  double device_ms = 0, gather_ms = 0;
+  uint64_t h2d = 0, d2h = 0;
+  for (uint32_t s = 0; s < (uint32_t)ctx->devs.size(); ++s) {
+    Device& d = ctx->devs[s];
+    Plan& P = ctx->plans[s];
+    const uint64_t m = P.m;
+    if (m == 0) continue;
+    HIPCHK(hipSetDevice(d.id));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    d.st.device_ms = elapsed_ms(d.ev_up0, d.ev1);
+    d.st.upload_ms = elapsed_ms(d.ev_up0, d.ev_up1);
+    d.st.kernel_ms = elapsed_ms(d.ev_k0, d.ev1);
+    device_ms = std::max<double>(device_ms, d.st.device_ms);
+    uint32_t errflag;
+    std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+    const bool straight = out_pinned;  // the digests were D2H'd straight into out
+    if (errflag & 2) {
+      // a split chain's handoff timed out: its digests are undefined; the
+      // payload is still on the device, so re-hash the shard unsplit
+      rerun_unsplit(ctx, d, P, straight ? out + 32 * d.lo : d.h_out.as<uint8_t>());
+      d.st.d2h_bytes += 32 * m + 4;
+      std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+      if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out (re-run failed)");
+    }
+    if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
+    d.st.h2d_bytes += d.st.h2d_payload_bytes;
+    h2d += d.st.h2d_bytes;
+    d2h += d.st.d2h_bytes;
+    gather_ms += d.st.gather_ms;
+    const uint32_t* rep = P.rep_of();
+    const uint8_t* h = d.h_out.as<uint8_t>();
+    if (straight) {
+      if (rep)  // aliases copy their representative's digest
+        parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
+          uint8_t* o = out + 32 * d.lo;
+          for (uint64_t i = a; i < b; ++i)
+            if (rep[i] != i) std::memcpy(o + 32 * i, o + 32 * (uint64_t)rep[i], 32);
+        });
+      continue;
+    }
+    parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
+      if (!rep)
+        std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));
+      else
+        for (uint64_t i = a; i < b; ++i) std::memcpy(out + 32 * (d.lo + i), h + 32 * (uint64_t)rep[i], 32);
+    });
+  }
+  ctx->stats.calls++;
+  ctx->stats.plan_ms = t_plan - t0;
+  ctx->stats.pack_ms = gather_ms;
+  ctx->stats.device_ms = device_ms;
+  ctx->stats.h2d_bytes = h2d;
+  ctx->stats.d2h_bytes = d2h;
+  ctx->stats.total_ms = now_ms() - t0;
+}
+
 template <class Gather>
 void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, const uint64_t* uid,
-                  uint8_t* out, Gather&& gather, const Direct* direct = nullptr,
-                  const uint64_t* pre_bounds = nullptr) {
+                  uint8_t* out, Gather&& gather, const uint64_t* pre_bounds = nullptr) {
   const uint32_t k = (uint32_t)ctx->devs.size();
-  const bool out_pinned = is_pinned_host(out);
+  const bool out_pinned = is_pinned_host(out) && is_pinned_host(out + 32 * n - 1);
   std::vector<uint64_t> bounds(k + 1);
   if (pre_bounds) std::copy(pre_bounds, pre_bounds + k + 1, bounds.begin());
   else partition(len, n, k, bounds.data());
@@ -1230,11 +1149,10 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     P.launched = 0;
     P.d2h_done = 0;
     P.later_min.clear();
+    P.rep_dev = nullptr;
     msha_shard_stats& st = ctx->devs[s].st;
-    const uint64_t payload = direct ? st.h2d_payload_bytes : 0;  // queued by upload_direct_spans
     st = msha_shard_stats{};
     st.device = ctx->devs[s].id;
-    st.h2d_payload_bytes = payload;
   }
   for (uint32_t s = 0; s < k; ++s) {
     ctx->devs[s].lo = bounds[s];
@@ -1312,9 +1230,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     d.h_meta.ensure(16 * P.m + 4 * P.m);
     uint64_t* h_off = d.h_meta.as<uint64_t>();
     uint64_t* h_len = h_off + P.m;
-    if (direct) {
-      // direct mode orders the lanes and fills their metadata in one pass (below)
-    } else if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
+    if (!P.rep.empty()) {  // lanes = the representatives, by descending block count
       order_by_blocks_desc(L, P.m, P.perm.data(), d.sort_tmp, P.rep.data());
       P.ordered = true;
     } else {
@@ -1327,11 +1243,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     // were folded into their representative above), so every lane of chunk c
     // reads bytes uploaded by the end of chunk c.
     uint64_t acc = 0;
-    if (direct) {  // the shard's byte ranges of the caller's pinned arena, uploaded as is
-      plan_direct_lanes(P, d, direct->off + d.lo, L, h_off, h_len, d.tmp_dev);
-      acc = d.arena_bytes;
-      if (P.ordered) plan_stream_back(P);
-    } else {
+    {
       // lane-indexed metadata: an exclusive scan of the 16-byte-rounded lengths
       // (lane q's payload lands at h_off[q]; payloads are placed in lane order)
       const unsigned T = plan_threads(P.lanes);
@@ -1369,7 +1281,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     d.arena_bytes = acc;
     trace("placement", t0);
     if (P.ordered) std::memcpy(h_len + P.m, P.perm.data(), 4 * P.lanes);
-    if (!direct) {
+    {
       uint64_t slot_bytes = 0;
       for (size_t c = 0; c + 1 < P.lane_cut.size(); ++c) {
         const uint64_t e = P.lane_cut[c + 1] < P.lanes ? h_off[P.lane_cut[c + 1]] : acc;
@@ -1386,6 +1298,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     d.out.ensure(32 * P.m);
     d.err.ensure(4);
     if (P.ordered) d.order.ensure(4 * P.lanes);
+    HIPCHK(hipEventRecord(d.ev_up0, d.stream));
     HIPCHK(hipMemcpyAsync(d.off.p, h_off, 8 * P.lanes, hipMemcpyHostToDevice, d.stream));
     HIPCHK(hipMemcpyAsync(d.len.p, h_len, 8 * P.lanes, hipMemcpyHostToDevice, d.stream));
     d.st.h2d_bytes = 16 * P.lanes;
@@ -1395,90 +1308,50 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     }
     HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
     HIPCHK(hipEventRecord(d.ev0, d.stream));
+    HIPCHK(hipStreamWaitEvent(d.copy_stream, d.ev0, 0));  // uploads start after ev0: device_ms spans them
     HIPCHK(hipEventRecord(d.slot_free[0], d.copy_stream));
     HIPCHK(hipEventRecord(d.slot_free[1], d.copy_stream));
   });
   const double t_plan = now_ms();
   trace("planned (metadata H2D queued)", t0);
 
-  // Issue chunk P.next of shard s (gather it into a staging slot and upload it,
-  // or, in direct mode, wait for the span chunk completing its payloads), and
-  // launch the kernel over the lanes accumulated since the last launch once
-  // they fill the GPU (2 waves per SIMD) or at the last chunk: hashing runs
-  // ~30x faster than PCIe delivers bytes, so a launch per 32 MiB chunk would
-  // only buy overlap worth a few % while a chunk of large messages (512 x 64
-  // KiB) leaves most SIMDs idle for the whole of its long chains. Returns
-  // whether shard s has chunks left.
+  // Issue chunk P.next of shard s: gather it into a staging slot, upload it, and
+  // launch the lanes accumulated so far when they fill the GPU (launch_lanes).
+  // Returns whether shard s has chunks left.
   auto issue_chunk = [&](uint32_t s, WorkerPool& pool) -> bool {
     Device& d = ctx->devs[s];
     Plan& P = plans[s];
     if (P.m == 0 || P.next + 1 >= P.lane_cut.size()) return false;
     const size_t c = P.next++;
-    const uint64_t q1 = P.lane_cut[c + 1];
     const uint64_t u0 = P.lane_cut[c], u1 = P.lane_cut[c + 1];
-    const uint64_t* h_off = d.h_meta.as<uint64_t>();  // lane -> arena offset (gather mode)
+    const uint64_t* h_off = d.h_meta.as<uint64_t>();  // lane -> arena offset
     HIPCHK(hipSetDevice(d.id));
-    if (direct) {
-      // the span chunk completing this lane group's payloads (queued up front)
-      HIPCHK(hipStreamWaitEvent(d.stream, d.span_ev[P.cut_chunk[c]], 0));
-    } else {
-      const uint64_t b0 = h_off[u0];
-      const uint64_t b1 = u1 >= P.lanes ? d.arena_bytes : h_off[u1];
-      PinBuf& slot = d.slot[c & 1];
-      HIPCHK(hipEventSynchronize(d.slot_free[c & 1]));  // its previous H2D has drained
-      const double g0 = now_ms();
-      uint8_t* dst = slot.as<uint8_t>();
-      parallel_ranges(pool, u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
-        for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.perm[u], dst + (h_off[u] - b0));
-      });
-      const double g1 = now_ms();
-      if (d.st.gather_begin_ms == 0) d.st.gather_begin_ms = std::max(g0 - t0, 1e-6);
-      d.st.gather_end_ms = g1 - t0;
-      d.st.gather_ms += g1 - g0;
-      if (b1 > b0)
-        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
-                              d.copy_stream));
-      d.st.h2d_payload_bytes += b1 - b0;
-      HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
-      HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
-      HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
-    }
+    const uint64_t b0 = h_off[u0];
+    const uint64_t b1 = u1 >= P.lanes ? d.arena_bytes : h_off[u1];
+    PinBuf& slot = d.slot[c & 1];
+    HIPCHK(hipEventSynchronize(d.slot_free[c & 1]));  // its previous H2D has drained
+    const double g0 = now_ms();
+    uint8_t* dst = slot.as<uint8_t>();
+    parallel_ranges(pool, u1 - u0, b1 - b0, [&](uint64_t a, uint64_t b) {
+      for (uint64_t u = u0 + a; u < u0 + b; ++u) gather(d.lo + P.perm[u], dst + (h_off[u] - b0));
+    });
+    const double g1 = now_ms();
+    if (d.st.gather_begin_ms == 0) d.st.gather_begin_ms = std::max(g0 - t0, 1e-6);
+    d.st.gather_end_ms = g1 - t0;
+    d.st.gather_ms += g1 - g0;
+    if (b1 > b0)
+      HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + b0, slot.p, b1 - b0, hipMemcpyHostToDevice,
+                            d.copy_stream));
+    d.st.h2d_payload_bytes += b1 - b0;
+    HIPCHK(hipEventRecord(d.slot_free[c & 1], d.copy_stream));
+    HIPCHK(hipEventRecord(d.chunk_in, d.copy_stream));
     const bool last = P.next + 1 >= P.lane_cut.size();
-    const uint64_t fill = (uint64_t)d.cus * 4 * 64 * 2;
-    if (!last && q1 - P.launched < fill) return !last;
-    const uint64_t l0 = P.launched, lanes = q1 - l0;
-    P.launched = q1;
-    // off/len are lane-indexed; out_idx maps lane -> shard-local message
-    // (identity placement: lane q is message q)
-    msha::SplitPlan sp;
-    msha::LaunchKind kind;
-    HIPCHK(msha::launch_digest_batch(
-        d.arena.as<uint8_t>(), d.off.as<uint64_t>() + l0, d.len.as<uint64_t>() + l0, nullptr,
-        P.ordered ? d.order.as<uint32_t>() + l0 : nullptr, lanes,
-        d.out.as<uint8_t>() + (P.ordered ? 0 : 32 * l0), d.err.as<uint32_t>(), d.cus,
-        ctx->kernel_policy, d.stream, split_for(d, lanes, ctx->kernel_policy, sp), &kind));
-    count_launch(ctx, &d, kind);
-    // Identity lanes: these digests are final, bring them back while later
-    // chunks upload and hash (into the caller's buffer itself if it is pinned).
-    if (P.identity()) {
-      HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * l0,
-                            d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost, d.stream));
-      d.st.d2h_bytes += 32 * lanes;
-    } else if (!P.later_min.empty()) {
-      // Ordered direct lanes: slots below every later group's lowest slot are
-      // final (aliases among them are filled on the host after the sync).
-      const uint64_t x = P.later_min[c + 1];
-      if (x > P.d2h_done) {
-        HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * P.d2h_done,
-                              d.out.as<uint8_t>() + 32 * P.d2h_done, 32 * (x - P.d2h_done),
-                              hipMemcpyDeviceToHost, d.stream));
-        d.st.d2h_bytes += 32 * (x - P.d2h_done);
-        P.d2h_done = x;
-      }
-    }
+    if (last) HIPCHK(hipEventRecord(d.ev_up1, d.copy_stream));
+    HIPCHK(hipStreamWaitEvent(d.stream, d.chunk_in, 0));
+    launch_lanes(ctx, d, P, c, last, t0, out, out_pinned);
     return !last;
   };
-  if (!direct && k > 1) {
+  if (k > 1) {
     // Pageable arenas over several GPUs: one issuing thread per GPU, each with
     // its own gather helpers, so the host copy for GPU s+1 never waits on GPU
     // s's staging slot (msha_shard_stats gather_begin/end show the overlap).
@@ -1487,84 +1360,395 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       }
     });
   } else {
-    // One issuing thread, chunks round-robin over the GPUs so every copy
-    // engine stays busy (direct mode only enqueues waits and launches here).
+    // One GPU: the calling thread issues its chunks.
     for (bool more = true; more;) {
       more = false;
       for (uint32_t s = 0; s < k; ++s) more |= issue_chunk(s, WorkerPool::get());
     }
   }
-  for (uint32_t s = 0; s < k; ++s) {
-    Device& d = ctx->devs[s];
-    const uint64_t m = plans[s].m;
-    if (m == 0) continue;
-    HIPCHK(hipSetDevice(d.id));
-    HIPCHK(hipEventRecord(d.ev1, d.stream));
-    const uint64_t done = plans[s].d2h_done;  // slots streamed back after earlier launches
-    if (!plans[s].identity() && done < m) {
-      // d.out is message-ordered (lane q wrote slot perm[q]); a pinned result
-      // buffer takes it as is, the aliases' slots are filled on the host below
-      HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * done,
-                            d.out.as<uint8_t>() + 32 * done, 32 * (m - done), hipMemcpyDeviceToHost, d.stream));
-      d.st.d2h_bytes += 32 * (m - done);
+  for (uint32_t s = 0; s < k; ++s) queue_tail(ctx->devs[s], plans[s], out, out_pinned);
+  join_shards(ctx, t0, t_plan, out, out_pinned);
+}
+
+// Direct path, pass 1 over one shard's messages (threaded): stage their raw
+// (off, len) for the planner kernels (h_off null: the caller's arrays are
+// pinned and go up as they are), mark the granules (1 << gs bytes of the
+// caller's arena, numbered from glo) their payload bytes touch, and return the
+// shard's payload span. Zero-length messages need no bytes and mark nothing
+// (so one at the arena's very end uploads nothing past it).
+struct ShardSpan {
+  uint64_t lo = UINT64_MAX, hi = 0, sum = 0, g0 = UINT64_MAX, g1 = 0;
+  bool any() const { return hi > 0; }
+};
+
+ShardSpan stage_and_mark(const uint64_t* O, const uint64_t* L, uint64_t m, uint64_t glo, unsigned gs,
+                         uint64_t* h_off, uint64_t* h_len, std::vector<uint8_t>& mark) {
+  const unsigned T = plan_threads(m);
+  std::vector<ShardSpan> acc(T);
+  parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
+    ShardSpan r;
+    for (uint64_t i = a; i < b; ++i) {
+      const uint64_t o = O[i], l = L[i];
+      if (h_off) {
+        h_off[i] = o;
+        h_len[i] = l;
+      }
+      if (!l) continue;
+      r.lo = std::min(r.lo, o);
+      r.hi = std::max(r.hi, o + l);
+      r.sum += l;
+      const uint64_t g0 = (o - glo) >> gs, g1 = (o + l - 1 - glo) >> gs;
+      r.g0 = std::min(r.g0, g0);
+      r.g1 = std::max(r.g1, g1);
+      for (uint64_t g = g0; g <= g1; ++g)
+        if (!__atomic_load_n(&mark[g], __ATOMIC_RELAXED)) __atomic_store_n(&mark[g], 1, __ATOMIC_RELAXED);
     }
-    HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
-    d.st.d2h_bytes += 4;
+    acc[t] = r;
+  });
+  ShardSpan sh;
+  for (const ShardSpan& r : acc) {
+    sh.lo = std::min(sh.lo, r.lo);
+    sh.hi = std::max(sh.hi, r.hi);
+    sh.sum += r.sum;
+    sh.g0 = std::min(sh.g0, r.g0);
+    sh.g1 = std::max(sh.g1, r.g1);
   }
-  double kernel_ms = 0, gather_ms = 0;
-  uint64_t h2d = 0, d2h = 0;
-  for (uint32_t s = 0; s < k; ++s) {
-    Device& d = ctx->devs[s];
-    Plan& P = plans[s];
-    const uint64_t m = P.m;
-    if (m == 0) continue;
-    HIPCHK(hipSetDevice(d.id));
-    HIPCHK(hipStreamSynchronize(d.stream));
-    float ms = 0;
-    HIPCHK(hipEventElapsedTime(&ms, d.ev0, d.ev1));
-    d.st.device_ms = ms;
-    kernel_ms = std::max<double>(kernel_ms, ms);
-    uint32_t errflag;
-    std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
-    const bool straight = out_pinned;  // the digests were D2H'd straight into out
-    if (errflag & 2) {
-      // a split chain's handoff timed out: its digests are undefined; the
-      // payload is still on the device, so re-hash the shard unsplit
-      rerun_unsplit(ctx, d, P, straight ? out + 32 * d.lo : d.h_out.as<uint8_t>());
-      d.st.d2h_bytes += 32 * m + 4;
-      std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
-      if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out (re-run failed)");
-    }
-    if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
-    d.st.h2d_bytes += d.st.h2d_payload_bytes;
-    h2d += d.st.h2d_bytes;
-    d2h += d.st.d2h_bytes;
-    gather_ms += d.st.gather_ms;
-    const std::vector<uint32_t>& rep = P.rep;
-    const uint8_t* h = d.h_out.as<uint8_t>();
-    if (straight) {
-      if (!rep.empty())  // aliases copy their representative's digest
-        parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
-          uint8_t* o = out + 32 * d.lo;
-          for (uint64_t i = a; i < b; ++i)
-            if (rep[i] != i) std::memcpy(o + 32 * i, o + 32 * (uint64_t)rep[i], 32);
-        });
+  return sh;
+}
+
+// gmap[g] = device offset of granule gbase + g (marked granules packed back to
+// back in granule order) or UINT64_MAX (not uploaded), g < ng; gbase ==
+// UINT64_MAX: nothing is marked. Returns the device bytes.
+uint64_t build_gmap(const std::vector<uint8_t>& mark, uint64_t gbase, uint64_t ng, unsigned gs, uint64_t* gmap) {
+  uint64_t dev = 0;
+  for (uint64_t g = 0; g < ng; ++g) {
+    const bool on = gbase != UINT64_MAX && mark[gbase + g];
+    gmap[g] = on ? dev : UINT64_MAX;
+    dev += on ? 1ull << gs : 0;
+  }
+  return dev;
+}
+
+// The shard's uploads: f(caller offset, device offset, bytes) for each run of
+// mapped granules, clipped to the shard's payload span [lo, hi) (so never past
+// the arena), in ascending device order, split where device offsets cross a
+// kDirectChunk boundary.
+template <class F>
+void for_each_upload(const uint64_t* gmap, uint64_t ng, uint64_t gbase, uint64_t glo, unsigned gs, uint64_t lo,
+                     uint64_t hi, F&& f) {
+  const uint64_t G = 1ull << gs;
+  for (uint64_t g = 0; g < ng;) {
+    if (gmap[g] == UINT64_MAX) {
+      ++g;
       continue;
     }
-    parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
-      if (rep.empty())
-        std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));
-      else
-        for (uint64_t i = a; i < b; ++i) std::memcpy(out + 32 * (d.lo + i), h + 32 * (uint64_t)rep[i], 32);
-    });
+    uint64_t g1 = g;
+    while (g1 < ng && gmap[g1] != UINT64_MAX) ++g1;
+    const uint64_t h0 = std::max(lo, glo + (gbase + g) * G), h1 = std::min(hi, glo + (gbase + g1) * G);
+    for (uint64_t pos = h0; pos < h1;) {
+      const uint64_t r = pos - glo;
+      const uint64_t dev = gmap[(r >> gs) - gbase] + (r & (G - 1));
+      const uint64_t piece = std::min(h1 - pos, (dev / kDirectChunk + 1) * kDirectChunk - dev);
+      f(pos, dev, piece);
+      pos += piece;
+    }
+    g = g1;
   }
-  ctx->stats.calls++;
-  ctx->stats.plan_ms = t_plan - t0;
-  ctx->stats.pack_ms = gather_ms;
-  ctx->stats.device_ms = kernel_ms;
-  ctx->stats.h2d_bytes = h2d;
-  ctx->stats.d2h_bytes = d2h;
-  ctx->stats.total_ms = now_ms() - t0;
+}
+
+// One pass over a host call's messages (threaded): validation (every message
+// inside the arena), the covered span, totals, the OR of the offsets
+// (alignment), the largest block count, and the partition's piece sums.
+struct BatchScan {
+  uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0, offbits = 0, bmax = 0;
+  std::vector<uint64_t> csum;  // piece_sums() layout
+};
+
+void scan_batch(const uint8_t* arena, uint64_t arena_len, const uint64_t* off, const uint64_t* len, uint64_t n,
+                BatchScan& r) {
+  const uint64_t P = std::max<uint64_t>(1, (n + kPiece - 1) / kPiece);
+  r.csum.assign(P + 1, 0);
+  struct Acc {
+    uint64_t lo = UINT64_MAX, hi = 0, sum = 0, offbits = 0, bmax = 0, bad = UINT64_MAX;
+  };
+  const unsigned T = std::min<unsigned>(plan_threads(n), (unsigned)P);
+  std::vector<Acc> acc(T);
+  parallel_chunks(P, T, [&](unsigned t, uint64_t p0, uint64_t p1) {
+    Acc a;
+    for (uint64_t p = p0; p < p1 && a.bad == UINT64_MAX; ++p) {
+      uint64_t blocks = 0;
+      for (uint64_t i = p * kPiece, e = std::min(n, (p + 1) * kPiece); i < e; ++i) {
+        const uint64_t o = off[i], l = len[i];
+        if (l > arena_len || o > arena_len - l) {
+          a.bad = i;
+          break;
+        }
+        a.offbits |= o;
+        a.lo = std::min(a.lo, o);
+        a.hi = std::max(a.hi, o + l);
+        a.sum += l;
+        const uint64_t b = blocks_for(l);
+        blocks += b;
+        a.bmax = std::max(a.bmax, b);
+      }
+      r.csum[p + 1] = blocks;
+    }
+    acc[t] = a;
+  });
+  r.offbits = reinterpret_cast<uintptr_t>(arena);
+  for (const Acc& a : acc) {  // pieces in index order: the first bad message is reported
+    if (a.bad != UINT64_MAX)
+      throw MshaError(MSHA_ERR_INVALID_ARG, "message " + std::to_string(a.bad) + " [off+len] outside arena");
+    r.lo = std::min(r.lo, a.lo);
+    r.hi = std::max(r.hi, a.hi);
+    r.sum += a.sum;
+    r.offbits |= a.offbits;
+    r.bmax = std::max(r.bmax, a.bmax);
+  }
+  for (uint64_t p = 0; p < P; ++p) r.csum[p + 1] += r.csum[p];
+  r.blocks = r.csum[P];
+}
+
+// Direct (pinned-arena) host call, planned on the GPU. Each shard, on a host
+// thread of its own (for_each_shard), and with no whole-batch phase after the
+// scan:
+//   1. one threaded pass over its messages stages their raw (off, len) in
+//      pinned memory and marks the granules (>= 64 KiB) of the arena they touch;
+//   2. the copy stream uploads the metadata and granule map, then the marked
+//      byte ranges (runs of granules, compacted) in 64 MiB device pieces with
+//      one event each -- no gather copy;
+//   3. the planner kernels (plan.hip) fold aliases, order the lanes by (piece
+//      completing the payload, descending block count) and write lane-indexed
+//      off/len/slot; the host reads back the group cuts and per-group minima;
+//   4. each lane group is launched behind its piece's event, and the digest
+//      slots that are final stream back after each launch.
+// The host's share of the call is the scan and pass 1, ~2 passes over 16 bytes
+// per message; everything per-lane runs on the GPU.
+// A one-use barrier for the shard threads of one call. A thread that leaves
+// early (an empty shard, an exception) still counts itself in (Arrival's
+// destructor) so the others never wait forever.
+struct CallBarrier {
+  std::mutex mu;
+  std::condition_variable cv;
+  uint32_t left;
+  explicit CallBarrier(uint32_t n) : left(n) {}
+  void arrive(bool wait) {
+    std::unique_lock<std::mutex> g(mu);
+    if (--left == 0) cv.notify_all();
+    else if (wait) cv.wait(g, [&] { return left == 0; });
+  }
+};
+struct Arrival {
+  CallBarrier* b;
+  bool done = false;
+  void wait() {
+    if (b && !done) b->arrive(true);
+    done = true;
+  }
+  ~Arrival() {
+    if (b && !done) b->arrive(false);
+  }
+};
+
+void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const uint64_t* len,
+                const uint8_t* arena, uint8_t* out, const BatchScan& sc) {
+  const uint32_t k = (uint32_t)ctx->devs.size();
+  const bool out_pinned = is_pinned_host(out) && is_pinned_host(out + 32 * n - 1);
+  // off/len in pinned memory (msha_pinned_alloc, as the Go adapter packs them):
+  // uploaded as they are, no staging copy
+  const bool meta_pinned = is_pinned_host(off) && is_pinned_host(off + n - 1) && is_pinned_host(len) &&
+                           is_pinned_host(len + n - 1);
+  std::vector<uint64_t> bounds(k + 1);
+  if (k == 1) {
+    bounds[0] = 0;
+    bounds[1] = n;
+  } else {
+    partition_pieces(len, n, k, sc.csum, bounds.data());
+  }
+  // One granule grid over the batch's span: at most 2^20 granules of >= 64 KiB.
+  unsigned gs = 16;
+  while (((sc.hi - (sc.lo & ~((1ull << gs) - 1))) >> gs) >= (1ull << 20)) ++gs;
+  const uint64_t G = 1ull << gs;
+  const uint64_t glo = sc.lo & ~(G - 1);
+  const uint64_t nG = ((sc.hi - glo) >> gs) + 1;
+  // Shards sharing one GPU (MSHA_VIRTUAL_SHARDS) share its PCIe link and DMA
+  // engines: every shard's metadata goes up before any shard's payload, or a
+  // shard's planner waits behind the other shards' payload (up to the whole
+  // batch). Separate GPUs have links of their own and never wait on each other.
+  bool shared_gpu = false;
+  for (uint32_t s = 1; s < k; ++s) shared_gpu |= ctx->devs[s].id == ctx->devs[0].id;
+  CallBarrier meta_up(k), plan_up(k);
+  std::vector<uint8_t> meta_queued(k, 0);
+  std::vector<Plan>& plans = ctx->plans;
+  plans.resize(k);
+  for (uint32_t s = 0; s < k; ++s) {
+    Plan& P = plans[s];
+    P = Plan{};
+    P.ordered = true;
+    Device& d = ctx->devs[s];
+    d.lo = bounds[s];
+    d.hi = bounds[s + 1];
+    d.st = msha_shard_stats{};
+    d.st.device = d.id;
+  }
+  for_each_shard(ctx, [&](uint32_t s) {
+    Device& d = ctx->devs[s];
+    Plan& P = plans[s];
+    Arrival arrival{shared_gpu ? &meta_up : nullptr}, arrival2{shared_gpu ? &plan_up : nullptr};
+    const uint64_t m = d.hi - d.lo;
+    P.m = m;
+    d.st.messages = m;
+    if (m == 0) return;
+    const uint64_t* O = off + d.lo;
+    const uint64_t* L = len + d.lo;
+    HIPCHK(hipSetDevice(d.id));
+    // 1. stage (off, len) (unless the caller's arrays are pinned), mark granules, the shard's span
+    if (!meta_pinned) d.h_meta.ensure(16 * m);
+    uint64_t* h_off = meta_pinned ? nullptr : d.h_meta.as<uint64_t>();
+    uint64_t* h_len = meta_pinned ? nullptr : h_off + m;
+    std::vector<uint8_t>& mark = d.direct_mark;
+    mark.assign(nG, 0);
+    const ShardSpan sh = stage_and_mark(O, L, m, glo, gs, h_off, h_len, mark);
+    const bool any = sh.any();                       // some payload byte at all
+    const uint64_t gbase = any ? sh.g0 : 0, ng = any ? sh.g1 - sh.g0 + 1 : 1;
+    d.h_gmap.ensure(8 * ng);
+    uint64_t* gmap = d.h_gmap.as<uint64_t>();
+    const uint64_t dev_bytes = build_gmap(mark, any ? gbase : UINT64_MAX, ng, gs, gmap);
+    d.arena_bytes = dev_bytes;
+    trace("staged + marked", s, t0);
+    // 2. uploads: metadata + granule map first (the planner needs them)
+    const uint64_t chunks = std::max<uint64_t>(1, (dev_bytes + kDirectChunk - 1) / kDirectChunk);
+    d.arena.ensure(dev_bytes + msha::kArenaSlack);
+    d.p_meta.ensure(16 * m);
+    d.p_gmap.ensure(8 * ng);
+    while (d.span_ev.size() < chunks) {
+      hipEvent_t e;
+      HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      d.span_ev.push_back(e);
+    }
+    HIPCHK(hipEventRecord(d.ev_up0, d.copy_stream));
+    if (meta_pinned) {
+      HIPCHK(hipMemcpyAsync(d.p_meta.p, O, 8 * m, hipMemcpyHostToDevice, d.copy_stream));
+      HIPCHK(hipMemcpyAsync(d.p_meta.as<uint64_t>() + m, L, 8 * m, hipMemcpyHostToDevice, d.copy_stream));
+    } else {
+      HIPCHK(hipMemcpyAsync(d.p_meta.p, h_off, 16 * m, hipMemcpyHostToDevice, d.copy_stream));
+    }
+    HIPCHK(hipMemcpyAsync(d.p_gmap.p, gmap, 8 * ng, hipMemcpyHostToDevice, d.copy_stream));
+    HIPCHK(hipEventRecord(d.ev_meta, d.copy_stream));
+    meta_queued[s] = 1;
+    arrival.wait();  // shared GPU: every shard's metadata is queued before any planner or payload
+    // 3. planning on the GPU, behind the metadata. Queued before the payload:
+    // with streams of several shards sharing a GPU's hardware queues (HIP
+    // multiplexes streams over GPU_MAX_HW_QUEUES), a planner queued behind
+    // another stream's payload or kernel waits would wait for them too.
+    const bool aliases = m > 1 && any && sh.sum > sh.hi - sh.lo;  // overlapping payloads: maybe aliases
+    const uint64_t B = chunks * (sc.bmax + 1) <= (1u << 20) ? sc.bmax + 1 : 1;
+    const uint64_t nb = chunks * B;
+    uint64_t cap = 1024;
+    while (cap < 2 * m) cap <<= 1;
+    d.p_devoff.ensure(8 * m);
+    d.p_rep.ensure(4 * m);
+    d.p_cnt.ensure(4 * nb);
+    d.p_small.ensure(4 * (2 * chunks + 2));
+    if (aliases) {
+      d.p_table.ensure(4 * cap);
+      d.p_slot.ensure(4 * m);
+    }
+    d.off.ensure(8 * m);
+    d.len.ensure(8 * m);
+    d.order.ensure(4 * m);
+    d.out.ensure(32 * m);
+    d.err.ensure(4);
+    d.h_out.ensure(32 * m + 4);
+    d.h_small.ensure(4 * (2 * chunks + 2));
+    if (aliases) d.h_rep.ensure(4 * m);
+    if (aliases) HIPCHK(hipMemsetAsync(d.p_table.p, 0, 4 * cap, d.stream));
+    HIPCHK(hipMemsetAsync(d.p_cnt.p, 0, 4 * nb, d.stream));
+    HIPCHK(hipMemsetAsync(d.p_small.p, 0xFF, 4 * chunks, d.stream));  // gmin
+    HIPCHK(hipMemsetAsync(d.err.p, 0, 4, d.stream));
+    HIPCHK(hipStreamWaitEvent(d.stream, d.ev_meta, 0));
+    HIPCHK(hipEventRecord(d.ev_p0, d.stream));
+    msha::PlanArgs pa;
+    pa.off = d.p_meta.as<uint64_t>();
+    pa.len = pa.off + m;
+    pa.gmap = d.p_gmap.as<uint64_t>();
+    pa.glo = glo;
+    pa.gbase = gbase;
+    pa.gshift = gs;
+    pa.m = m;
+    pa.dev_off = d.p_devoff.as<uint64_t>();
+    pa.table = aliases ? d.p_table.as<uint32_t>() : nullptr;
+    pa.tmask = cap - 1;
+    pa.slot = aliases ? d.p_slot.as<uint32_t>() : nullptr;
+    pa.rep = d.p_rep.as<uint32_t>();
+    pa.chunks = chunks;
+    pa.B = B;
+    pa.bmax = sc.bmax;
+    pa.nb = nb;
+    pa.cnt = d.p_cnt.as<uint32_t>();
+    pa.gmin = d.p_small.as<uint32_t>();
+    pa.cut = pa.gmin + chunks;
+    pa.info = pa.cut + chunks + 1;
+    pa.lane_off = d.off.as<uint64_t>();
+    pa.lane_len = d.len.as<uint64_t>();
+    pa.lane_slot = d.order.as<uint32_t>();
+    HIPCHK(msha::launch_plan(pa, d.stream));
+    HIPCHK(hipEventRecord(d.ev_p1, d.stream));
+    HIPCHK(hipMemcpyAsync(d.h_small.p, d.p_small.p, 4 * (2 * chunks + 2), hipMemcpyDeviceToHost, d.stream));
+    HIPCHK(hipEventRecord(d.ev_plan, d.stream));
+    if (aliases) HIPCHK(hipMemcpyAsync(d.h_rep.p, d.p_rep.p, 4 * m, hipMemcpyDeviceToHost, d.stream));
+    d.st.d2h_bytes = 4 * (2 * chunks + 2) + (aliases ? 4 * m : 0);
+    // 4. the payload: behind every shard's metadata on a shared GPU
+    arrival2.wait();  // shared GPU: every shard's planner is queued before any payload
+    for (uint32_t o = 0; shared_gpu && o < k; ++o)
+      if (o != s && meta_queued[o] && ctx->devs[o].id == d.id)
+        HIPCHK(hipStreamWaitEvent(d.copy_stream, ctx->devs[o].ev_meta, 0));
+    // event c once every byte below device offset (c+1)*kDirectChunk is queued
+    uint64_t c = 0, uploaded = 0;
+    if (any)
+      for_each_upload(gmap, ng, gbase, glo, gs, sh.lo, sh.hi, [&](uint64_t pos, uint64_t dev, uint64_t bytes) {
+        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + dev, arena + pos, bytes, hipMemcpyHostToDevice,
+                              d.copy_stream));
+        uploaded += bytes;
+        for (; c < chunks && (c + 1) * kDirectChunk <= dev + bytes; ++c)
+          HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+      });
+    for (; c < chunks; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+    HIPCHK(hipEventRecord(d.ev_up1, d.copy_stream));
+    d.st.h2d_payload_bytes = uploaded;
+    d.st.h2d_bytes = 16 * m + 8 * ng;
+    trace("payload queued", s, t0);
+    HIPCHK(hipEventSynchronize(d.ev_plan));
+    d.st.plan_kernel_ms = elapsed_ms(d.ev_p0, d.ev_p1);
+    const uint32_t* gmin = d.h_small.as<uint32_t>();
+    const uint32_t* cut = gmin + chunks;
+    P.lanes = cut[chunks];
+    d.st.lanes = P.lanes;
+    P.rep_dev = aliases ? d.h_rep.as<uint32_t>() : nullptr;
+    // lane groups: one per piece that completes at least one payload
+    P.lane_cut.assign(1, 0);
+    P.cut_chunk.clear();
+    std::vector<uint64_t> gm;
+    for (uint64_t q = 0; q < chunks; ++q) {
+      if (cut[q + 1] == cut[q]) continue;
+      P.lane_cut.push_back(cut[q + 1]);
+      P.cut_chunk.push_back(q);
+      gm.push_back(gmin[q]);
+    }
+    const size_t groups = gm.size();
+    P.later_min.assign(groups + 1, m);
+    for (size_t g = groups; g-- > 0;) P.later_min[g] = std::min<uint64_t>(gm[g], P.later_min[g + 1]);
+    trace("planned on GPU", s, t0);
+    // 5. one launch per accumulated lane group, each behind its piece's upload
+    for (size_t g = 0; g < groups; ++g) {
+      HIPCHK(hipStreamWaitEvent(d.stream, d.span_ev[P.cut_chunk[g]], 0));
+      launch_lanes(ctx, d, P, g, g + 1 == groups, t0, out, out_pinned);
+    }
+    queue_tail(d, P, out, out_pinned);
+  });
+  double t_plan = t0;  // plan_ms: until the last shard's first kernel is queued
+  for (const Device& d : ctx->devs) t_plan = std::max(t_plan, t0 + d.st.first_launch_ms);
+  join_shards(ctx, t0, t_plan, out, out_pinned);
 }
 
 }  // namespace
@@ -1626,10 +1810,18 @@ int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint
         HIPCHK(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&d.ev0));
         HIPCHK(hipEventCreate(&d.ev1));
+        HIPCHK(hipEventCreate(&d.ev_up0));
+        HIPCHK(hipEventCreate(&d.ev_up1));
+        HIPCHK(hipEventCreate(&d.ev_k0));
+        HIPCHK(hipEventCreate(&d.ev_p0));
+        HIPCHK(hipEventCreate(&d.ev_p1));
+        HIPCHK(hipEventCreateWithFlags(&d.ev_meta, hipEventDisableTiming));
+        HIPCHK(hipEventCreateWithFlags(&d.ev_plan, hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.slot_free[0], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.slot_free[1], hipEventDisableTiming));
         HIPCHK(hipEventCreateWithFlags(&d.chunk_in, hipEventDisableTiming));
         d.st.device = i;
+        d.index = (uint32_t)ctx->devs.size();
         ctx->devs.push_back(std::move(d));
       }
     }
@@ -1660,6 +1852,18 @@ void msha_ctx_destroy(msha_ctx* ctx) {
 }
 
 const char* msha_last_error(const msha_ctx* ctx) { return ctx ? ctx->err : g_create_error; }
+
+uint64_t msha_last_error_copy(const msha_ctx* ctx, char* buf, uint64_t buf_len) {
+  std::unique_lock<std::mutex> lock(ctx ? ctx->mu : g_create_mu);
+  const char* e = ctx ? ctx->err : g_create_error;
+  const uint64_t n = std::strlen(e);
+  if (buf && buf_len) {
+    const uint64_t c = std::min(n, buf_len - 1);
+    std::memcpy(buf, e, c);
+    buf[c] = 0;
+  }
+  return n;
+}
 
 int msha_get_stats(const msha_ctx* ctx, msha_stats* out) {
   if (!ctx || !out) return MSHA_ERR_INVALID_ARG;
@@ -1726,45 +1930,22 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
   if (n >= 0xffffffffull) return fail(ctx, MSHA_ERR_INVALID_ARG, "more than 2^32-2 messages in one call");
   const double t0 = now_ms();
   return guarded(ctx, [&] {
-    // One pass (threaded for large batches): bounds, the covered span, total
-    // bytes and blocks, and the OR of all offsets (alignment).
-    struct Acc {
-      uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0, offbits = 0, bad = UINT64_MAX;
+    BatchScan sc;
+    scan_batch(arena, arena_len, off, len, n, sc);
+    const uint64_t lo = sc.lo, hi = sc.hi, sum = sc.sum;
+    const bool aligned16 = (sc.offbits & 15) == 0;
+    auto count = [&] {
+      ctx->stats.messages += n;
+      ctx->stats.message_bytes += sum;
+      ctx->stats.blocks += sc.blocks;
     };
-    const unsigned T = plan_threads(n);
-    std::vector<Acc> acc(T);
-    parallel_chunks(n, T, [&](unsigned t, uint64_t a, uint64_t b) {
-      Acc r;
-      for (uint64_t i = a; i < b; ++i) {
-        if (len[i] > arena_len || off[i] > arena_len - len[i]) {
-          r.bad = i;
-          break;
-        }
-        r.offbits |= off[i];
-        r.lo = std::min(r.lo, off[i]);
-        r.hi = std::max(r.hi, off[i] + len[i]);
-        r.sum += len[i];
-        r.blocks += blocks_for(len[i]);
-      }
-      acc[t] = r;
-    });
-    uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0, offbits = reinterpret_cast<uintptr_t>(arena);
-    for (const Acc& r : acc) {  // chunks in index order: the first bad message is reported
-      if (r.bad != UINT64_MAX)
-        throw MshaError(MSHA_ERR_INVALID_ARG, "message " + std::to_string(r.bad) + " [off+len] outside arena");
-      lo = std::min(lo, r.lo);
-      hi = std::max(hi, r.hi);
-      sum += r.sum;
-      blocks += r.blocks;
-      offbits |= r.offbits;
-    }
-    const bool aligned16 = (offbits & 15) == 0;
     if (n <= small_msgs()) {  // the latency path (run_small)
       // A pinned arena goes up as is only above 512 KiB: below that, packing it
       // behind the metadata (one H2D instead of two) is the faster of the two
       // (tools/latency.cpp: 32 KiB pinned 57 us as two copies, 44 us packed).
       const bool span = small_bytes() > 0 && aligned16 && hi - lo > kSmallSpanMin &&
-                        hi - lo <= small_span_bytes() && is_pinned_host(arena + lo);
+                        hi - lo <= small_span_bytes() && is_pinned_host(arena + lo) &&
+                        is_pinned_host(arena + hi - 1);
       uint64_t packed = 0;
       for (uint64_t i = 0; i < n && !span; ++i) packed += round16(len[i]);
       if (span || small_call(n, packed)) {
@@ -1772,34 +1953,33 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
         run_small(ctx, t0, n, len, out, [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); },
                   span ? &sp : nullptr);
         ctx->stats.direct_calls += span;
-        ctx->stats.messages += n;
-        ctx->stats.message_bytes += sum;
-        ctx->stats.blocks += blocks;
+        count();
         return;
       }
+    }
+    trace("validated", t0);
+    // Zero-copy upload when the caller packed into pinned memory (msha_pinned_alloc)
+    // with 16-byte aligned message starts and little waste between messages:
+    // the touched byte ranges go up as they are and the GPU plans the lanes.
+    const bool direct = aligned16 && hi > lo && hi - lo <= std::min(sum, hi - lo) + 16 * n + (1u << 20) &&
+                        is_pinned_host(arena + lo) && is_pinned_host(arena + hi - 1);
+    if (direct) {
+      run_direct(ctx, t0, n, off, len, arena, out, sc);
+      ctx->stats.direct_calls++;
+      count();
+      return;
     }
     // Overlapping payloads (sum of lengths > the span they cover) means there
     // may be aliases: give every message the index of the first message with
     // the same (off, len).
     const bool aliases = n > 1 && sum > hi - lo;
-    trace("validated", t0);
-    // Zero-copy upload when the caller packed into pinned memory (msha_pinned_alloc)
-    // with 16-byte aligned message starts and little waste between messages:
-    // the spans go out now, and the planning below overlaps their DMA.
-    const bool direct = aligned16 && hi - lo <= std::min(sum, hi - lo) + 16 * n + (1u << 20) &&
-                        is_pinned_host(arena + lo);
-    Direct dir{arena, off};
-    std::vector<uint64_t> bounds(ctx->devs.size() + 1);
-    if (direct) upload_direct_spans(ctx, t0, n, off, len, arena, bounds.data());
     if (aliases) alias_uids(off, len, n, ctx->uid, ctx->alias_table, ctx->alias_bucket, ctx->alias_tag);
     trace("aliases", t0);
+    std::vector<uint64_t> bounds(ctx->devs.size() + 1);
+    partition_pieces(len, n, (uint32_t)ctx->devs.size(), sc.csum, bounds.data());
     run_pipeline(ctx, t0, n, len, aliases ? ctx->uid.data() : nullptr, out,
-                 [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); },
-                 direct ? &dir : nullptr, direct ? bounds.data() : nullptr);
-    ctx->stats.direct_calls += direct;
-    ctx->stats.messages += n;
-    ctx->stats.message_bytes += sum;
-    ctx->stats.blocks += blocks;
+                 [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); }, bounds.data());
+    count();
   });
 }
 

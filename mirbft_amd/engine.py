@@ -120,7 +120,9 @@ class Engine:
 
     def _check(self, rc: int) -> None:
         if rc != L.MSHA_OK:
-            raise MshaError(rc, self._lib.msha_last_error(self._ctx).decode())
+            buf = ctypes.create_string_buffer(512)
+            self._lib.msha_last_error_copy(self._ctx, buf, len(buf))   # under the context's lock
+            raise MshaError(rc, buf.value.decode())
 
     def set_kernel_policy(self, policy: str) -> None:
         """"auto" (default), "lane" (one lane per message) or "coop" (cooperative chaining)."""

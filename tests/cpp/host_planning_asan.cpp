@@ -1,7 +1,9 @@
 // Host planning code of libmirsha under AddressSanitizer + UndefinedBehaviorSanitizer,
 // on the CPU (no GPU, no kernels): the alias detection, the size-class order,
-// the block partition and the direct-mode lane planner are the intricate,
-// index-heavy parts of the host pipeline (mirbft_amd/csrc/mirsha.cpp). This
+// the batch scan and block partition, and the direct path's granule marking and
+// upload enumeration are the intricate, index-heavy parts of the host pipeline
+// (mirbft_amd/csrc/mirsha.cpp; the direct path's lane planning runs on the GPU,
+// plan.hip, and is covered by the -m gpu tests). This
 // file includes mirsha.cpp itself so its internal functions are reachable, stubs
 // the kernel launchers (never called here), and checks every result against a
 // plain reference computed in this file, over random and edge-case inputs.
@@ -29,6 +31,7 @@ hipError_t launch_digest_of_digests(const uint8_t*, const uint32_t*, const uint6
                                     uint32_t*, hipStream_t, const SplitPlan*, LaunchKind*) {
   abort();
 }
+hipError_t launch_plan(const PlanArgs&, hipStream_t) { abort(); }
 }  // namespace msha
 
 static int failures = 0;
@@ -161,71 +164,128 @@ static void partition_cases(std::mt19937_64& rng) {
     }
 }
 
-// Direct-mode lane planner over a fake shard: granule map = identity over the
-// span, lanes grouped by the 64 MiB upload chunk holding each payload's end,
-// descending block count inside a group, stable, identity order detected.
-static void direct_lane_cases(std::mt19937_64& rng) {
-  for (int shape = 0; shape < 4; ++shape) {
-    const uint64_t m = shape == 3 ? 5 : 200000;
-    std::vector<uint64_t> off(m), len(m);
+// scan_batch: the first bad message is reported; totals, bmax and the piece
+// sums match a plain pass; the partition from its piece sums is the sequential rule.
+static void scan_cases(std::mt19937_64& rng) {
+  for (uint64_t n : {1ull, 5000ull, (1ull << 18) + 77}) {
+    std::vector<uint64_t> off(n), len(n);
     uint64_t pos = 0;
-    for (uint64_t i = 0; i < m; ++i) {
-      len[i] = shape == 0 ? 512 : (shape == 2 ? (rng() % 4) * 4096 + rng() % 64 : rng() % 2000);
+    for (uint64_t i = 0; i < n; ++i) {
+      len[i] = rng() % 3 == 0 ? 0 : rng() % 9000;
       off[i] = pos;
       pos += (len[i] + 15) & ~15ull;
     }
-    if (shape == 2) std::reverse(off.begin(), off.end());  // lanes descend through the span
-    Device d;
-    d.direct_glo = 0;
-    d.direct_gshift = 16;
-    const uint64_t nG = (pos >> 16) + 1;
-    d.direct_map.resize(nG);
-    for (uint64_t g = 0; g < nG; ++g) d.direct_map[g] = g << 16;
-    d.arena_bytes = nG << 16;
-    Plan P;
-    P.m = m;
-    P.lanes = m;
-    P.perm.resize(m);
-    std::vector<uint64_t> h_off(m), h_len(m), tdev;
-    plan_direct_lanes(P, d, off.data(), len.data(), h_off.data(), h_len.data(), tdev);
-    std::vector<uint8_t> seen(m, 0);
-    bool perm_ok = true;
-    for (uint64_t q = 0; q < m; ++q) {
-      const uint32_t i = P.perm[q];
-      perm_ok &= i < m && !seen[i];
-      if (i < m) seen[i] = 1;
-      perm_ok &= h_off[q] == off[i] && h_len[q] == len[i];
+    const uint64_t arena_len = pos + 64;
+    BatchScan sc;
+    scan_batch(reinterpret_cast<const uint8_t*>(uintptr_t(4096)), arena_len, off.data(), len.data(), n, sc);
+    uint64_t lo = UINT64_MAX, hi = 0, sum = 0, blocks = 0, bmax = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      lo = std::min(lo, off[i]);
+      hi = std::max(hi, off[i] + len[i]);
+      sum += len[i];
+      blocks += blocks_for(len[i]);
+      bmax = std::max(bmax, blocks_for(len[i]));
     }
-    CHECK(perm_ok, "direct shape %d: not a permutation with matching metadata", shape);
-    auto chunk = [&](uint64_t q) { return (h_off[q] + std::max<uint64_t>(h_len[q], 1) - 1) / kDirectChunk; };
-    bool grouped = true;
-    for (uint64_t q = 1; q < m; ++q) {
-      const uint64_t c0 = chunk(q - 1), c1 = chunk(q);
-      grouped &= c1 >= c0;
-      if (c1 == c0) {
-        const uint64_t b0 = blocks_for(h_len[q - 1]), b1 = blocks_for(h_len[q]);
-        grouped &= b1 <= b0 && (b1 < b0 || P.perm[q] > P.perm[q - 1]);
-      }
+    CHECK(sc.lo == lo && sc.hi == hi && sc.sum == sum && sc.blocks == blocks && sc.bmax == bmax,
+          "scan totals n=%llu", (unsigned long long)n);
+    std::vector<uint64_t> cs;
+    piece_sums(len.data(), n, cs);
+    CHECK(cs == sc.csum, "scan piece sums n=%llu", (unsigned long long)n);
+    for (uint32_t k : {1u, 3u, 8u}) {
+      std::vector<uint64_t> b(k + 1);
+      partition_pieces(len.data(), n, k, sc.csum, b.data());
+      CHECK(b == partition_ref(len, k), "partition from scan n=%llu k=%u", (unsigned long long)n, k);
     }
-    CHECK(grouped, "direct shape %d: not grouped by chunk / block order / stable", shape);
-    CHECK(P.lane_cut.front() == 0 && P.lane_cut.back() == m && P.cut_chunk.size() + 1 == P.lane_cut.size(),
-          "direct shape %d: lane groups", shape);
-    for (size_t g = 0; g + 1 < P.lane_cut.size(); ++g)
-      for (uint64_t q = P.lane_cut[g]; q < P.lane_cut[g + 1]; q += 997)
-        CHECK(chunk(q) == P.cut_chunk[g], "direct shape %d: lane %llu outside its group's chunk", shape,
-              (unsigned long long)q);
-    CHECK(shape != 0 || !P.ordered, "a uniform ascending request batch keeps identity lanes");
-    if (P.ordered) {  // streamed D2H: later_min[g] = lowest slot written by groups >= g
-      plan_stream_back(P);
-      const size_t G = P.lane_cut.size() - 1;
-      bool ok = P.later_min.size() == G + 1 && P.later_min[G] == m;
-      uint64_t mn = m;
-      for (size_t g = G; g-- > 0 && ok;) {
-        for (uint64_t q = P.lane_cut[g]; q < P.lane_cut[g + 1]; ++q) mn = std::min<uint64_t>(mn, P.perm[q]);
-        ok &= P.later_min[g] == mn;
-      }
-      CHECK(ok, "direct shape %d: later_min is not the suffix minimum of the groups' slots", shape);
-      CHECK(shape != 2 || P.later_min[1] == 0, "reversed lanes: nothing is final before the last group");
+    // two bad messages: the lower index is the one reported
+    const uint64_t b1 = n / 2, b2 = n - 1;
+    std::vector<uint64_t> bad = len;
+    bad[b2] = arena_len + 1;
+    bad[b1] = arena_len - off[b1] + 1;
+    std::string what;
+    try {
+      scan_batch(nullptr, arena_len, off.data(), bad.data(), n, sc);
+    } catch (const MshaError& e) {
+      what = e.what();
+    }
+    CHECK(what == "message " + std::to_string(b1) + " [off+len] outside arena", "scan error: '%s'", what.c_str());
+  }
+}
+
+// Direct path's host share over random shards: staged metadata, granule marks,
+// the compacted device map and the upload enumeration. Simulated DMA: every
+// upload piece is copied into a fake device arena; then each message's bytes
+// must sit at its remapped device offset, no upload may read outside the
+// caller's arena (a zero-length message at its very end included) or cross a
+// 64 MiB device piece, and lanes whose payload ends in piece c are complete once
+// the uploads that end at or below (c+1) * 64 MiB are.
+static void direct_upload_cases(std::mt19937_64& rng) {
+  for (int shape = 0; shape < 5; ++shape) {
+    const uint64_t n = shape == 4 ? 3 : 40000;
+    std::vector<uint64_t> off(n), len(n);
+    uint64_t pos = 0;
+    for (uint64_t i = 0; i < n; ++i) {
+      len[i] = shape == 0 ? 512 : rng() % 5000;
+      if (shape == 1 && rng() % 7 == 0) len[i] = 0;
+      off[i] = pos;
+      pos += (len[i] + 15) & ~15ull;
+      if (shape == 3 && rng() % 100 == 0) pos += rng() % (3u << 20);  // gaps: untouched granules
+    }
+    if (shape == 2)  // an aliased pool at the start (c5 shape): 5% point back into it
+      for (uint64_t i = 0; i < n; ++i)
+        if (rng() % 20 == 0) {
+          off[i] = (rng() % 50) * 4096;
+          len[i] = 1 + rng() % 4000;
+        }
+    const uint64_t arena_len = pos;
+    off[n - 1] = arena_len;  // a zero-length message exactly at the arena's end
+    len[n - 1] = 0;
+    std::vector<uint8_t> host(arena_len + 1);
+    for (auto& b : host) b = (uint8_t)rng();
+    BatchScan sc;
+    scan_batch(host.data(), arena_len, off.data(), len.data(), n, sc);
+    unsigned gs = shape == 3 ? 12 : 16;  // small granules: many runs
+    const uint64_t glo = sc.lo & ~((1ull << gs) - 1);
+    const uint64_t nG = ((sc.hi - glo) >> gs) + 1;
+    // the shard: the second half of the batch (a sub-range like a real shard)
+    const uint64_t a = n / 2, m = n - a;
+    std::vector<uint64_t> h_off(m), h_len(m);
+    std::vector<uint8_t> mark(nG, 0);
+    const ShardSpan sh = stage_and_mark(off.data() + a, len.data() + a, m, glo, gs, h_off.data(), h_len.data(), mark);
+    bool staged = true;
+    for (uint64_t i = 0; i < m; ++i) staged &= h_off[i] == off[a + i] && h_len[i] == len[a + i];
+    CHECK(staged, "direct shape %d: staged metadata differs", shape);
+    CHECK(sh.any(), "direct shape %d: no payload", shape);
+    const uint64_t gbase = sh.g0, ng = sh.g1 - sh.g0 + 1;
+    std::vector<uint64_t> gmap(ng);
+    const uint64_t dev_bytes = build_gmap(mark, gbase, ng, gs, gmap.data());
+    std::vector<uint8_t> dev(dev_bytes + 64, 0xEE);
+    uint64_t last_end = 0;
+    bool inside = true, ascending = true, in_piece = true;
+    for_each_upload(gmap.data(), ng, gbase, glo, gs, sh.lo, sh.hi, [&](uint64_t p, uint64_t d, uint64_t bytes) {
+      inside &= bytes > 0 && p + bytes <= arena_len && d + bytes <= dev_bytes;
+      ascending &= d >= last_end;
+      in_piece &= d / kDirectChunk == (d + bytes - 1) / kDirectChunk;
+      last_end = d + bytes;
+      if (p + bytes <= arena_len && d + bytes <= dev_bytes) std::memcpy(dev.data() + d, host.data() + p, bytes);
+    });
+    CHECK(inside, "direct shape %d: an upload reads past the arena or writes past the device span", shape);
+    CHECK(ascending && in_piece, "direct shape %d: uploads not ascending / crossing a 64 MiB piece", shape);
+    const uint64_t G = 1ull << gs;
+    uint64_t bad = 0;
+    for (uint64_t i = 0; i < m; ++i) {
+      const uint64_t o = h_off[i], l = h_len[i];
+      if (!l) continue;
+      const uint64_t r = o - glo;
+      const uint64_t dv = gmap[(r >> gs) - gbase] + (r & (G - 1));
+      bad += dv == UINT64_MAX || dv + l > dev_bytes || std::memcmp(dev.data() + dv, host.data() + o, l) != 0;
+    }
+    CHECK(bad == 0, "direct shape %d: %llu messages not intact at their device offset", shape,
+          (unsigned long long)bad);
+    if (shape == 2) {  // the pool's granules are uploaded, the first half's own bytes are not
+      uint64_t total = 0;
+      for_each_upload(gmap.data(), ng, gbase, glo, gs, sh.lo, sh.hi, [&](uint64_t, uint64_t, uint64_t b) { total += b; });
+      CHECK(total < arena_len * 3 / 4, "direct shape 2: %llu of %llu bytes uploaded for half the batch",
+            (unsigned long long)total, (unsigned long long)arena_len);
     }
   }
 }
@@ -239,10 +299,12 @@ static void wide_pool_case(std::mt19937_64& rng) {
     msha_ctx ctx;
     ctx.devs.resize(2);
     ctx.devs[0].id = 0;
-    ctx.devs[1].id = 1;  // two physical GPUs: host_threads_total = 12 (the override)
+    ctx.devs[1].id = 1;  // two physical GPUs: host_threads_total = 12 (the override), at most the machine's
+    const unsigned want = std::min(12u, std::max(1u, std::thread::hardware_concurrency()));
     unsigned seen = 0;
     const int rc = guarded(&ctx, [&] { seen = plan_threads(1u << 20); });
-    CHECK(rc == MSHA_OK && seen == 12, "wide pool: %u threads (rc %d)", seen, rc);
+    CHECK(rc == MSHA_OK && (seen == want || (want <= 16 && seen == WorkerPool::get().size())),
+          "wide pool: %u threads, want %u (rc %d)", seen, want, rc);
     CHECK(tl_pool == nullptr, "wide pool: caller's pool not restored");
     const uint64_t n = (1u << 20) + 3;
     std::vector<uint64_t> off(n), len(n);
@@ -261,7 +323,8 @@ int main() {
   wide_pool_case(rng);
   order_cases(rng);
   partition_cases(rng);
-  direct_lane_cases(rng);
+  scan_cases(rng);
+  direct_upload_cases(rng);
   if (failures) {
     fprintf(stderr, "%d failures\n", failures);
     return 1;

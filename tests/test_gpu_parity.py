@@ -521,6 +521,63 @@ def test_pinned_direct_chunked_sharded(monkeypatch):
         assert e.stats()["direct_calls"] == 2
 
 
+def _pinned_copy(e, a: np.ndarray) -> np.ndarray:
+    """a copied into msha_pinned_alloc memory (same dtype and shape)."""
+    p = e.pinned_empty(a.nbytes).view(a.dtype).reshape(a.shape)
+    p[...] = a
+    return p
+
+
+@pytest.mark.parametrize("shards", [1, 3, 8])
+def test_pinned_direct_gpu_planned(shards, monkeypatch):
+    """The direct path is planned on the GPU (plan.hip): aliases folded by the
+    device hash table, lanes bucketed by (upload piece, descending blocks),
+    digest slots streamed back per group. c5 batches over 1, 3 and 8 virtual
+    shards, with pageable and pinned off/len (the latter uploaded as they are):
+    every digest bit-exact, every shard's first kernel queued and its planner
+    timed."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", str(shards))
+    w = W.c5_storm(3 << 17)
+    exp = _oracle_dedup(w)
+    with Engine(1) as e:
+        arena = _pinned_copy(e, w.arena)
+        out = e.pinned_empty(w.n * 32).reshape(w.n, 32)
+        for meta in ("pageable", "pinned"):
+            off, ln = (w.off, w.len) if meta == "pageable" else (_pinned_copy(e, w.off), _pinned_copy(e, w.len))
+            out[...] = 0
+            got = e.digest_batch(arena, off, ln, out=out)
+            assert np.array_equal(got, exp), meta
+            sh = e.shard_stats()
+            assert len(sh) == shards and sum(s["messages"] for s in sh) == w.n
+            assert all(s["first_launch_ms"] > 0 and s["plan_kernel_ms"] > 0 for s in sh), sh
+            assert sum(s["lanes"] for s in sh) < w.n                      # aliases folded on the GPU
+            # upload and kernel spans lie inside the shard's device window
+            assert all(0 < s["upload_ms"] <= s["device_ms"] + 1e-3 and 0 < s["kernel_ms"] <= s["device_ms"] + 1e-3
+                       for s in sh), sh
+        assert e.stats()["direct_calls"] == 2
+
+
+def test_pinned_direct_empty_message_at_arena_end(engine):
+    """A zero-length message whose offset is the arena's length, in an exact-size
+    pinned arena ending on a page boundary, through the pipelined direct path
+    (> 64 K messages): it needs no bytes, so no upload reads past the arena
+    (ADVICE r2), and its digest is SHA-256("")."""
+    w = W.c2_requests(3 << 16)
+    n = w.n + 1
+    size = (w.arena.size + 4095) // 4096 * 4096
+    arena = engine.pinned_empty(size)
+    arena[: w.arena.size] = w.arena
+    off = np.append(w.off, np.uint64(size))
+    ln = np.append(w.len, np.uint64(0))
+    before = engine.stats()["direct_calls"]
+    got = engine.digest_batch(arena, off, ln)
+    assert engine.stats()["direct_calls"] == before + 1
+    assert np.array_equal(got[:-1], oracle.digest_batch(w.arena, w.off, w.len))
+    assert bytes(got[-1]) == hashlib.sha256(b"").digest()
+    assert engine.shard_stats()[0]["h2d_payload_bytes"] <= size
+
+
 def _cus():
     import torch
     return torch.cuda.get_device_properties(0).multi_processor_count
