@@ -71,14 +71,8 @@ def parse():
                         "STRIDE 0 makes every lane hash the same cached message)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=10.0)
-    p.add_argument("--e2e", action="store_true",
-                   help="instead: time the HOST entry point (pack + PCIe H2D + kernel + D2H) on the "
-                        "same workload; prints an end-to-end line (never the headline value)")
     p.add_argument("--policy", default="auto", choices=["auto", "lane", "coop"],
                    help="batch-kernel policy (msha_set_kernel_policy); digests are identical")
-    p.add_argument("--pinned", action="store_true",
-                   help="with --e2e: the batch is packed in pinned host memory (msha_pinned_alloc), "
-                        "as a cgo adapter would, so the library DMAs it as is")
     p.add_argument("--events", default="span", choices=["step", "span"],
                    help="span: one HIP event pair around the K launches (default); step: a pair "
                         "around every launch (costs c3 8%% per step: the A/B of the events' cost)")
@@ -89,7 +83,8 @@ def parse():
                         "one libmirsha context over N GPUs (device_mask) and the host entry point "
                         "msha_digest_batch on a pinned arena (end-to-end, PCIe-inclusive)")
     p.add_argument("--pageable", action="store_true", help="with --mode lib: a pageable numpy arena")
-    p.add_argument("--no-extra", action="store_true", help="skip the extra_configs (c3, c4, c5) legs")
+    p.add_argument("--no-extra", action="store_true",
+                   help="skip the extra_configs legs (one GPU: c3, c4, c5; N GPUs: c5 over all ranks)")
     p.add_argument("--no-host-api", action="store_true",
                    help="skip the host_api leg (c5 through msha_digest_batch over all N GPUs, one process)")
     return p.parse_args()
@@ -148,7 +143,7 @@ def cpu_baseline(w, seconds: float):
     off, ln = w.off[:n], w.len[:n]
     per = int(ln.sum())
     v, g, done, el = _time_cpu(lambda: oracle.digest_batch(w.arena, off, ln), n, per, seconds / 2)
-    line = {"value": None, "unit": "digests/s", "cores": 1, "kind": "port", "gbps": None,
+    line = {"value": None, "unit": "digests/s", "cores": 1, "kind": "port", "impl": None, "gbps": None,
             "scalar_port": {"value": v, "gbps": g, "source": "oracle/sha256_oracle.c, plain scalar C, 1 thread"},
             "sample": f"first {n} messages of the same workload, repeated for {el:.1f} s "
                       f"({done} digests) per leg"}
@@ -162,6 +157,8 @@ def cpu_baseline(w, seconds: float):
         # goroutine, mirbft.go:470) with the fastest SHA-256 this host has (OpenSSL,
         # SHA-NI): Go 1.15's AVX2 crypto/sha256 would be slower, the scalar port slower still
         line["value"], line["gbps"] = v1, g1
+        line["impl"] = ("openssl-sha-ni-1-thread (proxy for Go crypto/sha256): the oracle's restatement of "
+                        "serial.go:180-198 in C over OpenSSL EVP SHA-256, oracle/sha256_openssl.c")
         m = min(w.n, 4096 * CPU_THREADS)
         offm, lnm = w.off[:m], w.len[:m]
         vt, gt, _, _ = _time_cpu(lambda: oracle.openssl_digest_batch(w.arena, offm, lnm, CPU_THREADS), m,
@@ -175,6 +172,7 @@ def cpu_baseline(w, seconds: float):
     except (OSError, RuntimeError) as e:   # libcrypto missing: report the port only
         line["openssl"] = {"error": str(e)}
         line["value"], line["gbps"] = v, g
+        line["impl"] = "scalar C restatement of serial.go:180-198 over FIPS 180-4, oracle/sha256_oracle.c"
     return line
 
 
@@ -257,8 +255,10 @@ def host_api_leg(args, world: int) -> dict:
             "value": d["value"], "unit": "digests/s", "n_gpus": d["n_gpus"], "shards": d["shards"],
             "virtual_shards": d["virtual_shards"], "ms_per_call": d["ms_per_step"],
             "gbps_hashed": d["gbps_hashed"], "steps": d["steps"], "plan_ms": d["last_call_stats"]["plan_ms"],
-            "per_gpu": [{"device": x["device"], "messages": x["messages"], "h2d_bytes": x["h2d_bytes"],
-                         "device_ms": x["device_ms"]} for x in d["last_call_shards"]]}
+            "first_launch_ms_max": max(x["first_launch_ms"] for x in d["last_call_shards"]),
+            "per_gpu": [{k: x[k] for k in ("device", "messages", "lanes", "h2d_bytes", "device_ms", "upload_ms",
+                                           "kernel_ms", "first_launch_ms", "plan_kernel_ms")}
+                        for x in d["last_call_shards"]]}
 
 
 def kind_of(st0: dict, st1: dict) -> str:
@@ -396,6 +396,39 @@ def extra_config(eng, cfg: str, args, dev, stream) -> dict:
     return out
 
 
+def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist) -> dict:
+    """BASELINE config c5 as quoted -- the node's 2^23-action storm split over the
+    job's GPUs (strong scaling: each rank hashes its 2^23 / N slice, the same
+    generator stream bench.py's one-GPU c5 leg uses) -- kernel-resident, timed
+    like the headline: barrier + synchronize around K launches per rank, the max
+    over ranks. Every rank verifies 512 of its digests against the oracle."""
+    import torch
+    w = build_workload("c5", rank, world)
+    step, d_out = kernel_step(eng, w, "c5", dev, stream)
+    st0 = eng.stats()
+    elapsed, kern_ms, warm, _ = time_steps(step, args, dev, stream, barrier=dist.barrier)
+    dist.barrier()
+    eng.device_status()
+    kind = kind_of(st0, eng.stats())
+    verify_sample(w, d_out)
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kern_max = (float(x) for x in t.tolist())
+    tot = torch.tensor([w.n, w.message_bytes, w.blocks], dtype=torch.float64)
+    dist.all_reduce(tot)
+    n, nbytes, blocks = (float(x) for x in tot.tolist())
+    del step, d_out
+    torch.cuda.empty_cache()
+    achieved = OPS_PER_BLOCK * blocks / (kern_max * 1e-3) / 1e12      # all GPUs, slowest rank's launch
+    return {"workload": f"c5: {1 << 23} mixed actions (70/25/5) over {world} GPUs, {w.n} per GPU",
+            "n_gpus": world, "scaling": "strong", "value": n * args.steps / elapsed, "unit": "digests/s",
+            "gbps_hashed": nbytes * args.steps / elapsed / 1e9, "ms_per_step": elapsed / args.steps * 1e3,
+            "kernel_ms_mean_max_over_ranks": kern_max, "kernel": kind,
+            "frac": achieved / (PEAK_VALU_TOPS * world), "achieved": achieved, "peak": PEAK_VALU_TOPS * world,
+            "blocks": int(blocks), "verified": "512 digests per rank vs oracle (stride not a multiple of 64)",
+            "warmup_steps_run": warm}
+
+
 def run_lib(args):
     """North-star host path in one process: one libmirsha context over N GPUs
     (device_mask, or MSHA_VIRTUAL_SHARDS shards of one GPU), batch packed in a
@@ -481,8 +514,6 @@ def main():
     eng = Engine(1 << local)
     eng.set_kernel_policy(args.policy)
     w = build_workload(args.config, rank, world)
-    if args.e2e:
-        return run_e2e(args, eng, w, world)
     # A dedicated stream: the launches and the timing events share it (torch's
     # default stream has handle 0, which the C ABI reads as "context stream").
     stream = torch.cuda.Stream(dev)
@@ -537,13 +568,21 @@ def main():
             del step, d_out
             torch.cuda.empty_cache()
             line["extra_configs"] = {c: extra_config(eng, c, args, dev, stream) for c in ("c3", "c4", "c5")}
-        if not args.no_cpu_baseline and world == 1:
-            line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
+    if world > 1 and args.config == "c2" and not args.no_extra:
+        # every rank takes part: c5 is quoted over the node's GPUs (BASELINE config 5)
+        del step, d_out
+        torch.cuda.empty_cache()
+        c5 = extra_c5_ranks(eng, args, dev, stream, rank, world, dist)
+        if rank == 0:
+            line["extra_configs"] = {"c5": c5}
     eng.close()
     if world > 1:
         dist.barrier()              # every rank has released its GPU
         dist.destroy_process_group()
     if rank == 0:
+        if not args.no_cpu_baseline:
+            # on the host cores, after every rank has released its GPU
+            line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
         if not args.no_host_api:
             line["host_api"] = host_api_leg(args, world)
         print(json.dumps(line), flush=True)

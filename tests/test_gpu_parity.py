@@ -249,7 +249,13 @@ def test_c2_full_size_bit_exact(engine):
     w = W.c2_requests()
     d_arena, d_off, d_len = _to_dev(w)
     out = torch.empty((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    before = engine.stats()
     engine.digest_batch_device(d_arena, d_off, d_len, out)
+    engine.device_status()
+    # the kernel bench.py times for c2: one lane per message, nothing else
+    st = engine.stats()
+    assert st["launches_lane"] == before["launches_lane"] + 1
+    assert all(st[k] == before[k] for k in ("launches_pipe", "launches_coop", "launches_split"))
     out2 = torch.empty_like(out)
     engine.digest_uniform_device(d_arena, w.uniform_stride, 512, w.n, out2)
     engine.device_status()
@@ -267,11 +273,20 @@ def test_c3_full_size_bit_exact(engine):
     idx = torch.from_numpy(w.idx.view(np.int32)).to(dev)
     begin = torch.from_numpy(w.begin.view(np.int64)).to(dev)
     out = torch.empty((w.n, 32), dtype=torch.uint8, device=dev)
+    before = engine.stats()
     engine.digest_of_digests_device(table, idx, begin, out)
+    engine.device_status()
+    # bench.py's c3dd and c3 legs time split chaining (3 full waves per SIMD + a
+    # surplus): a planner change that moved either form off it would fail here
+    mid = engine.stats()
+    assert mid["launches_split"] == before["launches_split"] + 1 and mid["launches_dod"] == before["launches_dod"]
     d_arena, d_off, d_len = _to_dev(w)
     out2 = torch.empty_like(out)
     engine.digest_batch_device(d_arena, d_off, d_len, out2)
     engine.device_status()
+    st = engine.stats()
+    assert st["launches_split"] == mid["launches_split"] + 1
+    assert all(st[k] == mid[k] for k in ("launches_lane", "launches_pipe", "launches_coop"))
     exp = oracle.digest_batch(w.arena, w.off, w.len)
     assert np.array_equal(out.cpu().numpy(), exp)
     assert np.array_equal(out2.cpu().numpy(), exp)

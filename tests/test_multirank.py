@@ -80,8 +80,8 @@ def test_bench_two_ranks_on_the_engine():
     import subprocess
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--share-device",
-                        "--steps", "5", "--warmup", "2", "--min-warmup-ms", "50", "--no-cpu-baseline"],
-                       env=env, capture_output=True, text=True, timeout=240)
+                        "--steps", "5", "--warmup", "2", "--min-warmup-ms", "50", "--cpu-seconds", "1.5"],
+                       env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     lines = [l for l in r.stdout.splitlines() if l.strip()]
     assert len(lines) == 1, r.stdout
@@ -91,3 +91,11 @@ def test_bench_two_ranks_on_the_engine():
     assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["kernel"] == want
     assert "error" not in d["host_api"] and d["host_api"]["shards"] == 2
     assert d["value"] > 0 and d["config"]["messages_per_gpu"] == 1 << 20
+    # BASELINE config 5 as quoted: the 2^23 storm over both ranks, kernel-resident, verified
+    c5 = d["extra_configs"]["c5"]
+    assert c5["n_gpus"] == 2 and c5["scaling"] == "strong" and c5["value"] > 0 and 0 < c5["frac"] < 1
+    assert c5["blocks"] > 0 and "512 digests per rank" in c5["verified"]
+    # the CPU baseline at N > 1 too (rank 0, after the ranks released their GPUs)
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0 and cb["impl"]
+    assert d["host_api"]["first_launch_ms_max"] > 0
