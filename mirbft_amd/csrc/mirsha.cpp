@@ -215,6 +215,7 @@ struct Device {
   hipEvent_t chunk_in = nullptr;                 // last chunk's bytes are on the device
   std::vector<hipEvent_t> span_ev;               // direct mode: upload piece c is on the device
   DevBuf arena, off, len, order, out, err, idx, begin, table;
+  // pinned staging, allocated with this GPU current (the runtime's pool for its NUMA node)
   PinBuf h_arena, h_meta, h_out, slot[2];
   // small-call path (run_small): [meta | payload] in, [error word | digests] out
   DevBuf sm_in, sm_out;
@@ -1165,6 +1166,10 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
     P.m = d.hi - d.lo;
     d.st.messages = P.m;
     if (P.m == 0) return;
+    // this GPU current before any staging allocation: without
+    // hipHostMallocNumaUser the runtime takes pinned memory from the host pool
+    // of the current device's nearest CPU agent (its NUMA node)
+    HIPCHK(hipSetDevice(d.id));
     const uint64_t* L = len + d.lo;
     // Aliases (same uid) have identical bytes, hence identical digests: only
     // the first message of each uid gets a lane; the others copy its digest
