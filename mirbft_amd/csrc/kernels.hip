@@ -356,6 +356,9 @@ __device__ __forceinline__ void hash_blocks(State& s, const uint8_t* p, uint64_t
 // [b0, b1).
 struct ArenaSrc {  // messages arena[off[m] : off[m]+len[m]] (k_digest_batch's form)
   static constexpr int kMinWaves = 8;  // occupancy hint (__launch_bounds__): <= 64 VGPRs
+  // segment waves fetch their first block before the handoff wait (fits in the
+  // 64 VGPRs: SGPR spills to VGPR lanes only)
+  static constexpr bool kPreload = true;
   const uint8_t* arena;
   const uint64_t* off;
   const uint64_t* len;
@@ -387,9 +390,26 @@ struct ArenaSrc {  // messages arena[off[m] : off[m]+len[m]] (k_digest_batch's f
     g.ok = seg == 0 ? check_aligned(g.p, g.slot, err) : (reinterpret_cast<uintptr_t>(g.p) & 15) == 0;
     return g;
   }
+  // The finished words of block b (byte-swapped, or the padded tail / length block).
+  __device__ __forceinline__ void preload(const Msg& g, uint32_t b, uint32_t (&w)[16]) const {
+    const uint32_t nfull = (uint32_t)(g.len >> 6);
+    if (b <= nfull) load_block16(g.p + 64 * (uint64_t)b, w);
+    if (b < nfull) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    } else if (b == nfull) {
+      uint32_t rr = (uint32_t)(g.len & 63);
+      asm volatile("" : "+v"(rr));
+      build_tail(w, rr, g.len, w);
+    } else {
+      length_block(g.len, w);
+    }
+  }
+  // Blocks [b0, b1); block b0's words w0 were preloaded (before the handoff wait).
   __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1,
-                                         const Beat& beat) const {
-    for (uint32_t c = b0; c < b1; c += kBeatBlocks) {
+                                         const Beat& beat, uint32_t (&w0)[16]) const {
+    compress(st, w0);
+    for (uint32_t c = b0 + 1; c < b1; c += kBeatBlocks) {
       hash_blocks(st, g.p, g.len, c, std::min(c + kBeatBlocks, b1));
       beat(c);
     }
@@ -443,6 +463,9 @@ struct DigestSrc {
   // allows 6). That still hides the loads: the compression loop's issue rate is
   // flat from 2 to 8 waves, and Batch launches run ~3 per SIMD.
   static constexpr int kMinWaves = 5;
+  // no early fetch: the held block costs this kernel 2 VGPR spills (c3dd 92.1 ->
+  // 92.9-93.2 us, profiles/r03_ab_c3_preload/)
+  static constexpr bool kPreload = false;
   const uint8_t* table;
   const uint32_t* idx;
   const uint64_t* begin;
@@ -548,13 +571,16 @@ struct DigestSrc {
     g.ok = true;
     return g;
   }
+  __device__ __forceinline__ void preload(const Msg& g, uint32_t b, uint32_t (&w)[16]) const {
+    const uint4* tab = reinterpret_cast<const uint4*>(table);
+    if (b < g.cnt / 2) dod_pair_block(tab, idx + g.k0, 2 * (uint64_t)b, w);
+    else dod_final_block(tab, idx + g.k0, 2 * (uint64_t)b, g.cnt, w);
+  }
   __device__ __forceinline__ void blocks(const Msg& g, State& st, uint32_t b0, uint32_t b1,
                                          const Beat& beat) const {
-    const uint4* tab = reinterpret_cast<const uint4*>(table);
     uint32_t w[16];
     for (uint32_t b = b0; b < b1; ++b) {
-      if (b < g.cnt / 2) dod_pair_block(tab, idx + g.k0, 2 * (uint64_t)b, w);
-      else dod_final_block(tab, idx + g.k0, 2 * (uint64_t)b, g.cnt, w);
+      preload(g, b, w);
       compress(st, w);
       if (b % kBeatBlocks == 0) beat(b);  // spill-free here (53 VGPRs)
     }
@@ -577,6 +603,25 @@ __global__ __launch_bounds__(256, Src::kMinWaves) void k_digest_split(Src src, u
   const uint32_t lane = threadIdx.x & 63;
   uint64_t* flag = sp.flags + chain;
   const uint64_t ep = split_word(sp.epoch, 0, 0);
+  // Everything that does not depend on the previous segment is fetched before
+  // waiting for it: the message's metadata and this segment's first block (into
+  // registers: the acquire below invalidates the caches), so the handoff costs
+  // the flag and the 32-byte state, not a payload round trip as well.
+  const uint64_t i = sp.n_main + (uint64_t)chain * 64 + lane;
+  typename Src::Msg g{};
+  uint32_t b0 = 0, b1 = 0;
+  uint32_t w0[Src::kPreload ? 16 : 1];
+  const bool mine = i < n;
+  if (mine) {
+    g = src.open(i, seg, out);
+    if (g.ok) {
+      b0 = (uint32_t)((uint64_t)g.nb * seg / sp.segments);
+      b1 = (uint32_t)((uint64_t)g.nb * (seg + 1) / sp.segments);
+      if constexpr (Src::kPreload) {
+        if (b0 < b1) src.preload(g, b0, w0);
+      }
+    }
+  }
   if (seg > 0) {  // wait until seg segments of this chain are done (same launch: same epoch)
     uint64_t t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t prev = t0;
@@ -603,28 +648,25 @@ __global__ __launch_bounds__(256, Src::kMinWaves) void k_digest_split(Src src, u
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   }
   const Beat beat{flag, split_word(sp.epoch, seg, 0)};
-  const uint64_t i = sp.n_main + (uint64_t)chain * 64 + lane;
-  if (i < n) {
-    const typename Src::Msg g = src.open(i, seg, out);
-    if (g.ok) {
-      const uint32_t b0 = (uint32_t)((uint64_t)g.nb * seg / sp.segments);
-      const uint32_t b1 = (uint32_t)((uint64_t)g.nb * (seg + 1) / sp.segments);
-      State st;
-      if (seg == 0) {
-        state_init(st);
-      } else {  // the previous segment's state, parked in this message's digest slot
-        const uint4 lo = reinterpret_cast<const uint4*>(g.slot)[0];
-        const uint4 hi = reinterpret_cast<const uint4*>(g.slot)[1];
-        st.h[0] = lo.x; st.h[1] = lo.y; st.h[2] = lo.z; st.h[3] = lo.w;
-        st.h[4] = hi.x; st.h[5] = hi.y; st.h[6] = hi.z; st.h[7] = hi.w;
-      }
-      src.blocks(g, st, b0, b1, beat);
-      if (seg + 1 == sp.segments) {
-        store_digest(st, g.slot);
-      } else {  // raw state words, resumed by the next segment
-        reinterpret_cast<uint4*>(g.slot)[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
-        reinterpret_cast<uint4*>(g.slot)[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
-      }
+  if (mine && g.ok) {
+    State st;
+    if (seg == 0) {
+      state_init(st);
+    } else {  // the previous segment's state, parked in this message's digest slot
+      const uint4 lo = reinterpret_cast<const uint4*>(g.slot)[0];
+      const uint4 hi = reinterpret_cast<const uint4*>(g.slot)[1];
+      st.h[0] = lo.x; st.h[1] = lo.y; st.h[2] = lo.z; st.h[3] = lo.w;
+      st.h[4] = hi.x; st.h[5] = hi.y; st.h[6] = hi.z; st.h[7] = hi.w;
+    }
+    if (b0 < b1) {  // (a segment may have no block)
+      if constexpr (Src::kPreload) src.blocks(g, st, b0, b1, beat, w0);
+      else src.blocks(g, st, b0, b1, beat);
+    }
+    if (seg + 1 == sp.segments) {
+      store_digest(st, g.slot);
+    } else {  // raw state words, resumed by the next segment
+      reinterpret_cast<uint4*>(g.slot)[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
+      reinterpret_cast<uint4*>(g.slot)[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
     }
   }
   if (seg + 1 < sp.segments && !(seg == 0 && chain == sp.stall_chain)) {
@@ -872,13 +914,16 @@ static inline int split_mode(const SplitPlan& sp, int cus) {
 
 // Split chaining (AUTO and LANE) when the launch is q >= 1 full rounds of waves
 // over the SIMDs plus a surplus of r <= SIMDs/2 waves: r chains of
-// clamp(SIMDs / r, 2, kMaxSegments) segments, so no SIMD carries more than one
-// segment. MSHA_SPLIT_SEGS overrides the cap for A/B (profiles/r01_ab_segs/).
-constexpr int kMaxSegments = 8;
-
-bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp) {
+// clamp(SIMDs / r, 2, cap) segments, so no SIMD carries more than one segment.
+// The cap (kernels.hpp): arena messages 12 -- their segment waves fetch their
+// first block before the handoff wait, which makes a handoff cheap enough for
+// more, shorter segments (c3 90.0 -> 88.3-88.9 us; 8 / 10 / 12 / 14 / 16:
+// 89.5-90.0 / 89.9 / 88.3-88.9 / 88.9-89.3 / 89.5-89.6, profiles/r03_ab_c3_preload/);
+// digest-of-digests 8 (profiles/r01_ab_segs/). MSHA_SPLIT_SEGS overrides both (A/B).
+bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp, int cap) {
   static const int forced = env_int("MSHA_SPLIT", -1);  // A/B: 0 = never
-  static const int max_segs = std::min(64, std::max(2, env_int("MSHA_SPLIT_SEGS", kMaxSegments)));
+  static const int forced_segs = env_int("MSHA_SPLIT_SEGS", 0);
+  const int max_segs = std::min(64, std::max(2, forced_segs > 0 ? forced_segs : cap));
   static const uint64_t min_q = (uint64_t)std::max(1, env_int("MSHA_SPLIT_MIN_Q", 1));  // A/B
   if (forced == 0 || policy == 2) return false;
   const uint64_t simds = (uint64_t)cus * 4;

@@ -27,7 +27,10 @@ struct SplitPlan {
   uint64_t* flags = nullptr;  // device, >= chains entries, one word per chain:
                               // epoch | segments done | progress beat (kernels.hip)
 };
-bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp);
+// Segment caps of split chaining: arena messages / digest-of-digests (kernels.hip).
+constexpr int kMaxSegmentsArena = 12;
+constexpr int kMaxSegmentsDod = 8;
+bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp, int cap);
 
 // Which kernel a launcher ran (msha_stats launch counters; tests assert them).
 enum LaunchKind { kLaunchNone = 0, kLaunchLane, kLaunchPipe, kLaunchCoop, kLaunchSplit, kLaunchDod };

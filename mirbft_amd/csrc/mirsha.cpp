@@ -265,8 +265,9 @@ struct Device {
 // Consecutive launches use different flag arrays of a ring and unique epochs,
 // so a launch never reads another launch's flags.
 constexpr uint64_t kSplitRing = 16;
-const msha::SplitPlan* split_for(Device& d, uint64_t n, int policy, msha::SplitPlan& sp) {
-  if (!msha::plan_split(n, d.cus, policy, &sp)) return nullptr;
+const msha::SplitPlan* split_for(Device& d, uint64_t n, int policy, msha::SplitPlan& sp,
+                                 int cap = msha::kMaxSegmentsArena) {
+  if (!msha::plan_split(n, d.cus, policy, &sp, cap)) return nullptr;
   const uint64_t per = (uint64_t)d.cus * 2;  // plan_split: chains <= SIMDs / 2
   if (!d.split_flags) {
     HIPCHK(hipMalloc(&d.split_flags, kSplitRing * per * sizeof(uint64_t)));
@@ -2102,7 +2103,8 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
       HIPCHK(msha::launch_digest_of_digests(d.table.as<uint8_t>(), d.idx.as<uint32_t>(),
                                             d.begin.as<uint64_t>(), m, d.out.as<uint8_t>(),
                                             d.err.as<uint32_t>(), d.stream,
-                                            split_for(d, m, ctx->kernel_policy, sp), &kind));
+                                            split_for(d, m, ctx->kernel_policy, sp, msha::kMaxSegmentsDod),
+                                            &kind));
       count_launch(ctx, &d, kind);
       HIPCHK(hipEventRecord(d.ev1, d.stream));
       d.h_out.ensure(32 * m + 4);
@@ -2211,7 +2213,8 @@ int msha_digest_of_digests_device(msha_ctx* ctx, const uint8_t* d_table, const u
     msha::SplitPlan sp;
     msha::LaunchKind kind;
     HIPCHK(msha::launch_digest_of_digests(d_table, d_idx, d_begin, n, d_out, d.err.as<uint32_t>(), st,
-                                          split_for(d, n, ctx->kernel_policy, sp), &kind));
+                                          split_for(d, n, ctx->kernel_policy, sp, msha::kMaxSegmentsDod),
+                                          &kind));
     count_launch(ctx, nullptr, kind);
   });
 }

@@ -17,7 +17,7 @@
 
 namespace msha {
 // Kernel launchers are GPU code (kernels.hip); the host planning never launches.
-bool plan_split(uint64_t, int, int, SplitPlan*) { return false; }
+bool plan_split(uint64_t, int, int, SplitPlan*, int) { return false; }
 hipError_t launch_digest_batch(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*,
                                const uint32_t*, uint64_t, uint8_t*, uint32_t*, int, int, hipStream_t,
                                const SplitPlan*, LaunchKind*) {
