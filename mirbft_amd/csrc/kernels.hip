@@ -664,13 +664,21 @@ __global__ __launch_bounds__(256, Src::kMinWaves) void k_digest_split(Src src, u
     }
     if (seg + 1 == sp.segments) {
       store_digest(st, g.slot);
-    } else {  // raw state words, resumed by the next segment
-      reinterpret_cast<uint4*>(g.slot)[0] = make_uint4(st.h[0], st.h[1], st.h[2], st.h[3]);
-      reinterpret_cast<uint4*>(g.slot)[1] = make_uint4(st.h[4], st.h[5], st.h[6], st.h[7]);
+    } else {  // raw state words, resumed by the next segment: written through (sc1)
+      uint64_t* q = reinterpret_cast<uint64_t*>(g.slot);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __hip_atomic_store(q + j, ((uint64_t)st.h[2 * j + 1] << 32) | st.h[2 * j], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  // Hand-off (cdna_hip_programming.md Guideline 16, R1): the state went out
+  // write-through (sc1), so no release fence (buffer_wbl2 sc1 would write back
+  // the XCD L2's every dirty line -- the main waves' digests among them -- at
+  // 1.7-6.5 us per hand-off); this wave drains its stores, then one lane stores
+  // the flag. The next segment polls it relaxed and takes ONE agent acquire.
   if (seg + 1 < sp.segments && !(seg == 0 && chain == sp.stall_chain)) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (lane == 0)
       __hip_atomic_store(flag, split_word(sp.epoch, seg + 1, 0), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
@@ -915,11 +923,13 @@ static inline int split_mode(const SplitPlan& sp, int cus) {
 // Split chaining (AUTO and LANE) when the launch is q >= 1 full rounds of waves
 // over the SIMDs plus a surplus of r <= SIMDs/2 waves: r chains of
 // clamp(SIMDs / r, 2, cap) segments, so no SIMD carries more than one segment.
-// The cap (kernels.hpp): arena messages 12 -- their segment waves fetch their
-// first block before the handoff wait, which makes a handoff cheap enough for
-// more, shorter segments (c3 90.0 -> 88.3-88.9 us; 8 / 10 / 12 / 14 / 16:
-// 89.5-90.0 / 89.9 / 88.3-88.9 / 88.9-89.3 / 89.5-89.6, profiles/r03_ab_c3_preload/);
-// digest-of-digests 8 (profiles/r01_ab_segs/). MSHA_SPLIT_SEGS overrides both (A/B).
+// The cap (kernels.hpp) is 12 for both sources since round 3 made a hand-off
+// cheap -- the arena segment's first block fetched before its wait, the state
+// handed over write-through with no release fence: c3 8 / 10 / 12 / 14 / 16
+// segments 89.5-90.0 / 89.9 / 88.3-88.9 / 88.9-89.3 / 89.5-89.6 us
+// (profiles/r03_ab_c3_preload/); c3dd 92.3 -> 90.3 us at 12, 91.2 at 16, 93.9
+// at 24 (profiles/r03_ab_split_sc1/; 8 before, profiles/r01_ab_segs/).
+// MSHA_SPLIT_SEGS overrides both (A/B).
 bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp, int cap) {
   static const int forced = env_int("MSHA_SPLIT", -1);  // A/B: 0 = never
   static const int forced_segs = env_int("MSHA_SPLIT_SEGS", 0);

@@ -29,7 +29,7 @@ struct SplitPlan {
 };
 // Segment caps of split chaining: arena messages / digest-of-digests (kernels.hip).
 constexpr int kMaxSegmentsArena = 12;
-constexpr int kMaxSegmentsDod = 8;
+constexpr int kMaxSegmentsDod = 12;
 bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp, int cap);
 
 // Which kernel a launcher ran (msha_stats launch counters; tests assert them).
