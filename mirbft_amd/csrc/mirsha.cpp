@@ -331,9 +331,10 @@ uint64_t order_by_blocks_desc(const uint64_t* len, uint64_t n, uint32_t* order,
   });
   const uint64_t bmax = *std::max_element(tmax.begin(), tmax.end());
   if (bmax <= (1u << 20)) {
-    // per-thread histograms only while they stay small
-    const unsigned T = bmax <= (1u << 16) ? T0 : 1;
+    // per-thread histograms only while all of them together stay small (at most
+    // 2^20 counters: a wide pool of 128 threads must not zero and scan 128 x 64 K)
     const uint64_t B = bmax + 1;               // bucket j = block count bmax - j
+    const unsigned T = (unsigned)std::max<uint64_t>(1, std::min<uint64_t>(T0, (1u << 20) / B));
     std::vector<uint64_t> cnt((uint64_t)T * B, 0);
     parallel_chunks(n, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
       uint64_t* c = cnt.data() + (uint64_t)t * B;

@@ -573,6 +573,73 @@ def test_pinned_direct_gpu_planned(shards, monkeypatch):
         assert e.stats()["direct_calls"] == 2
 
 
+def _pinned_batch(e, lens, offs=None, seed=21):
+    """A pinned arena holding messages of the given lengths (16-byte aligned starts
+    unless offs is given) and the oracle's digests."""
+    lens = np.asarray(lens, dtype=np.uint64)
+    if offs is None:
+        offs = np.zeros(lens.size, dtype=np.uint64)
+        offs[1:] = np.cumsum((lens + np.uint64(15)) & ~np.uint64(15))[:-1]
+    offs = np.asarray(offs, dtype=np.uint64)
+    size = int((offs + lens).max()) + 64
+    host = W.random_bytes(seed, 0, size)
+    arena = e.pinned_empty(size)
+    arena[:] = host
+    w = W.Workload("planner-edge", host, offs, lens)
+    return arena, w, _oracle_dedup(w)
+
+
+def test_gpu_planner_edge_cases(engine):
+    """The GPU lane planner (plan.hip) on the shapes its fast paths do not cover:
+    (a) every message one payload (one lane, all others aliases);
+    (b) 4,096 distinct block counts in one 4,096-message tile, so the LDS key table
+        (1,024 slots) overflows and lanes fall back to the global counters;
+    (c) a 64 MiB message among 70,000 requests: pieces x (bmax + 1) > 2^20
+        counters, so lanes are bucketed by upload piece only;
+    (d) zero-length messages everywhere (and a shard of nothing else, below)."""
+    # (a) 100,000 actions on one 300-byte payload (+ one other)
+    lens = np.full(100_001, 300, dtype=np.uint64)
+    offs = np.zeros(100_001, dtype=np.uint64)
+    offs[-1] = 320
+    arena, w, exp = _pinned_batch(engine, lens, offs)
+    before = engine.stats()["direct_calls"]
+    assert np.array_equal(engine.digest_batch(arena, w.off, w.len), exp)
+    assert engine.shard_stats()[0]["lanes"] == 2
+    # (b) lengths i * 64 + 5: block counts 1 .. 4,096, all distinct, in one tile
+    i = np.arange(4096, dtype=np.uint64)
+    arena, w, exp = _pinned_batch(engine, i * np.uint64(64) + np.uint64(5), seed=22)
+    assert np.array_equal(engine.digest_batch(arena, w.off, w.len), exp)
+    # (c) two 64 MiB messages among 70,000 x 512 B
+    lens = np.full(70_002, 512, dtype=np.uint64)
+    lens[7] = lens[50_000] = 64 << 20
+    arena, w, exp = _pinned_batch(engine, lens, seed=23)
+    assert np.array_equal(engine.digest_batch(arena, w.off, w.len), exp)
+    # (d) every third message empty
+    lens = np.full(90_000, 700, dtype=np.uint64)
+    lens[::3] = 0
+    arena, w, exp = _pinned_batch(engine, lens, seed=24)
+    assert np.array_equal(engine.digest_batch(arena, w.off, w.len), exp)
+    assert engine.stats()["direct_calls"] == before + 4
+
+
+def test_gpu_planner_shard_of_empty_messages(monkeypatch):
+    """Over 3 virtual shards, a batch whose middle third is zero-length messages
+    only: that shard uploads nothing and hashes SHA-256("") for every one."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", "3")
+    lens = np.full(300_000, 50, dtype=np.uint64)      # 1 block each, like an empty message:
+    lens[100_000:200_000] = 0                         # the partition cuts at 100,000 and 200,000
+    with Engine(1) as e:
+        arena, w, exp = _pinned_batch(e, lens, seed=25)
+        got = e.digest_batch(arena, w.off, w.len)
+        assert np.array_equal(got, exp)
+        assert bytes(got[150_000]) == hashlib.sha256(b"").digest()
+        sh = e.shard_stats()
+        assert len(sh) == 3 and e.stats()["direct_calls"] == 1
+        assert [s["messages"] for s in sh] == [100_000] * 3, sh
+        assert sh[1]["h2d_payload_bytes"] == 0 and sh[0]["h2d_payload_bytes"] > 0, sh
+
+
 def test_pinned_direct_empty_message_at_arena_end(engine):
     """A zero-length message whose offset is the arena's length, in an exact-size
     pinned arena ending on a page boundary, through the pipelined direct path
