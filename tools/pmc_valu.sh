@@ -23,7 +23,7 @@ has() { [[ " $PASSES " == *" $1 "* ]]; }
 for spec in ${SPECS:-c2:auto c3:auto c3dd:auto c4:auto c5:auto ub_16384_65536:coop ub_16384_65536:lane}; do
   cfg=${spec%%:*}; pol=${spec##*:}; arg=$(echo $cfg | tr '_' ':')
   name=${cfg}_${pol}
-  cmd="python3 bench.py --config $arg --policy $pol --steps 3 --warmup 1 --no-cpu-baseline --no-extra"
+  cmd="python3 bench.py --config $arg --policy $pol --steps 3 --warmup 1 --no-cpu-baseline --no-extra --no-host-api"
   has sq && prof ${name}_sq "$SQ" $cmd
   has sq2 && prof ${name}_sq2 "$SQ2" $cmd
   has fetch && prof ${name}_fetch FETCH_SIZE $cmd
