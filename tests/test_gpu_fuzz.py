@@ -35,10 +35,10 @@ def _lengths(rng, n):
     return ln
 
 
-def _layout(rng, ln):
+def _layout(rng, ln, kind=None):
     """Offsets for lengths ln in an arena; returns (arena_size, off)."""
     n = ln.size
-    kind = rng.integers(0, 5)
+    kind = rng.integers(0, 5) if kind is None else kind
     align = 16 if kind in (0, 3, 4) else 1
     steps = (ln + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
     if kind == 1:                                   # unaligned gaps
@@ -119,3 +119,37 @@ def test_random_hash_actions_and_batches(engine, seed, monkeypatch):
     idx = rng.integers(0, table.shape[0], int(begin[-1]), dtype=np.uint32)
     got = engine.digest_of_digests(table, idx, begin)
     assert np.array_equal(got, oracle.digest_of_digests(table, idx, begin))
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_random_direct_gpu_planned(seed, monkeypatch):
+    """The pinned (direct) path, whose lanes the GPU plans (plan.hip): random
+    16-byte aligned layouts -- packed, aliased back into the batch, reversed, with
+    empty messages and a few large ones -- over 1 to 8 virtual shards, with the
+    off/len arrays pageable or pinned (uploaded as they are), every digest
+    against the oracle and the call counted as direct."""
+    from mirbft_amd import Engine
+    rng = np.random.default_rng(3000 + seed)
+    monkeypatch.setenv("MSHA_SMALL_BYTES", "0")                 # never the latency path
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", str(1 + seed % 8))
+    n = int(rng.choice([70_000, 130_000, 200_000]))
+    ln = _lengths(rng, n)
+    size, off = _layout(rng, ln, kind=int(rng.choice([0, 3, 4])))  # the 16-byte aligned layouts
+    data = rng.integers(0, 256, size + 64, dtype=np.uint8)
+    exp = _expect(data, off, ln)
+    with Engine(1) as e:
+        arena = e.pinned_empty(data.size)
+        arena[:] = data
+        if seed % 2:
+            po = e.pinned_empty(off.nbytes).view(np.uint64)
+            pl = e.pinned_empty(ln.nbytes).view(np.uint64)
+            po[:], pl[:] = off, ln
+            off_in, ln_in = po, pl
+        else:
+            off_in, ln_in = off, ln
+        got = e.digest_batch(arena, off_in, ln_in)
+        direct = e.stats()["direct_calls"]
+    assert np.array_equal(got, exp), (seed, n)
+    lo, hi, total = int(off.min()), int((off + ln).max()), int(ln.sum())
+    dense = hi > lo and hi - lo <= min(total, hi - lo) + 16 * n + (1 << 20)    # msha_digest_batch's rule
+    assert direct == int(dense), (direct, dense)
