@@ -1073,57 +1073,64 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
-// Wait for every shard of the call, re-run a shard whose split chain timed
-// out, fill the aliases' digests (each copies its representative's) and record
-// the call's figures: device_ms = first upload .. last kernel, upload_ms = first
-// .. last upload, kernel_ms = first kernel .. last kernel (HIP events).
-void join_shards(msha_ctx* ctx, double t0, double t_plan, uint8_t* out, bool out_pinned) {
+// Finish shard s of a host call, on the shard's own thread (shards finish side
+// by side): wait for its stream, re-run it unsplit if a split chain's hand-off
+// timed out, fill its aliases' digests (each copies its representative's) and
+// complete its msha_shard_stats: device_ms = first upload .. last kernel,
+// upload_ms = first .. last upload, kernel_ms = first kernel .. last (HIP events).
+void finish_shard(msha_ctx* ctx, uint32_t s, uint8_t* out, bool out_pinned) {
+  Device& d = ctx->devs[s];
+  Plan& P = ctx->plans[s];
+  const uint64_t m = P.m;
+  if (m == 0) return;
+  HIPCHK(hipSetDevice(d.id));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  d.st.device_ms = elapsed_ms(d.ev_up0, d.ev1);
+  d.st.upload_ms = elapsed_ms(d.ev_up0, d.ev_up1);
+  d.st.kernel_ms = elapsed_ms(d.ev_k0, d.ev1);
+  uint32_t errflag;
+  std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+  const bool straight = out_pinned;  // the digests were D2H'd straight into out
+  if (errflag & 2) {
+    // a split chain's handoff timed out: its digests are undefined; the
+    // payload is still on the device, so re-hash the shard unsplit
+    rerun_unsplit(ctx, d, P, straight ? out + 32 * d.lo : d.h_out.as<uint8_t>());
+    d.st.d2h_bytes += 32 * m + 4;
+    std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
+    if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out (re-run failed)");
+  }
+  if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
+  d.st.h2d_bytes += d.st.h2d_payload_bytes;
+  const uint32_t* rep = P.rep_of();
+  const uint8_t* h = d.h_out.as<uint8_t>();
+  if (straight) {
+    if (rep)  // aliases copy their representative's digest
+      parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
+        uint8_t* o = out + 32 * d.lo;
+        for (uint64_t i = a; i < b; ++i)
+          if (rep[i] != i) std::memcpy(o + 32 * i, o + 32 * (uint64_t)rep[i], 32);
+      });
+    return;
+  }
+  parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
+    if (!rep)
+      std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));
+    else
+      for (uint64_t i = a; i < b; ++i) std::memcpy(out + 32 * (d.lo + i), h + 32 * (uint64_t)rep[i], 32);
+  });
+}
+
+// The call's figures (msha_stats) from its finished shards'.
+void call_stats(msha_ctx* ctx, double t0, double t_plan) {
   double device_ms = 0, gather_ms = 0;
   uint64_t h2d = 0, d2h = 0;
   for (uint32_t s = 0; s < (uint32_t)ctx->devs.size(); ++s) {
-    Device& d = ctx->devs[s];
-    Plan& P = ctx->plans[s];
-    const uint64_t m = P.m;
-    if (m == 0) continue;
-    HIPCHK(hipSetDevice(d.id));
-    HIPCHK(hipStreamSynchronize(d.stream));
-    d.st.device_ms = elapsed_ms(d.ev_up0, d.ev1);
-    d.st.upload_ms = elapsed_ms(d.ev_up0, d.ev_up1);
-    d.st.kernel_ms = elapsed_ms(d.ev_k0, d.ev1);
-    device_ms = std::max<double>(device_ms, d.st.device_ms);
-    uint32_t errflag;
-    std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
-    const bool straight = out_pinned;  // the digests were D2H'd straight into out
-    if (errflag & 2) {
-      // a split chain's handoff timed out: its digests are undefined; the
-      // payload is still on the device, so re-hash the shard unsplit
-      rerun_unsplit(ctx, d, P, straight ? out + 32 * d.lo : d.h_out.as<uint8_t>());
-      d.st.d2h_bytes += 32 * m + 4;
-      std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
-      if (errflag & 2) throw MshaError(MSHA_ERR_HIP, "split-chain handoff timed out (re-run failed)");
-    }
-    if (errflag) throw MshaError(MSHA_ERR_ALIGNMENT, "internal: misaligned staged message");
-    d.st.h2d_bytes += d.st.h2d_payload_bytes;
-    h2d += d.st.h2d_bytes;
-    d2h += d.st.d2h_bytes;
-    gather_ms += d.st.gather_ms;
-    const uint32_t* rep = P.rep_of();
-    const uint8_t* h = d.h_out.as<uint8_t>();
-    if (straight) {
-      if (rep)  // aliases copy their representative's digest
-        parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
-          uint8_t* o = out + 32 * d.lo;
-          for (uint64_t i = a; i < b; ++i)
-            if (rep[i] != i) std::memcpy(o + 32 * i, o + 32 * (uint64_t)rep[i], 32);
-        });
-      continue;
-    }
-    parallel_chunks(m, plan_threads(m), [&](unsigned, uint64_t a, uint64_t b) {
-      if (!rep)
-        std::memcpy(out + 32 * (d.lo + a), h + 32 * a, 32 * (b - a));
-      else
-        for (uint64_t i = a; i < b; ++i) std::memcpy(out + 32 * (d.lo + i), h + 32 * (uint64_t)rep[i], 32);
-    });
+    if (ctx->plans[s].m == 0) continue;
+    const msha_shard_stats& st = ctx->devs[s].st;
+    device_ms = std::max(device_ms, st.device_ms);
+    gather_ms += st.gather_ms;
+    h2d += st.h2d_bytes;
+    d2h += st.d2h_bytes;
   }
   ctx->stats.calls++;
   ctx->stats.plan_ms = t_plan - t0;
@@ -1373,8 +1380,11 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
       for (uint32_t s = 0; s < k; ++s) more |= issue_chunk(s, WorkerPool::get());
     }
   }
-  for (uint32_t s = 0; s < k; ++s) queue_tail(ctx->devs[s], plans[s], out, out_pinned);
-  join_shards(ctx, t0, t_plan, out, out_pinned);
+  for_each_shard(ctx, [&](uint32_t s) {
+    queue_tail(ctx->devs[s], plans[s], out, out_pinned);
+    finish_shard(ctx, s, out, out_pinned);
+  });
+  call_stats(ctx, t0, t_plan);
 }
 
 // Direct path, pass 1 over one shard's messages (threaded): stage their raw
@@ -1752,10 +1762,11 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
       launch_lanes(ctx, d, P, g, g + 1 == groups, t0, out, out_pinned);
     }
     queue_tail(d, P, out, out_pinned);
+    finish_shard(ctx, s, out, out_pinned);
   });
   double t_plan = t0;  // plan_ms: until the last shard's first kernel is queued
   for (const Device& d : ctx->devs) t_plan = std::max(t_plan, t0 + d.st.first_launch_ms);
-  join_shards(ctx, t0, t_plan, out, out_pinned);
+  call_stats(ctx, t0, t_plan);
 }
 
 }  // namespace
