@@ -1398,39 +1398,55 @@ struct ShardSpan {
   bool any() const { return hi > 0; }
 };
 
-ShardSpan stage_and_mark(const uint64_t* O, const uint64_t* L, uint64_t m, uint64_t glo, unsigned gs,
-                         uint64_t* h_off, uint64_t* h_len, std::vector<uint8_t>& mark) {
+template <bool kStage>
+ShardSpan stage_and_mark_t(const uint64_t* O, const uint64_t* L, uint64_t m, uint64_t glo, unsigned gs,
+                           uint64_t* h_off, uint64_t* h_len, std::vector<uint8_t>& mark) {
   const unsigned T = plan_threads(m);
   std::vector<ShardSpan> acc(T);
   parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
-    ShardSpan r;
+    uint64_t lo = UINT64_MAX, hi = 0, sum = 0;
+    uint64_t last = UINT64_MAX;  // the granule this thread marked last
     for (uint64_t i = a; i < b; ++i) {
       const uint64_t o = O[i], l = L[i];
-      if (h_off) {
+      if (kStage) {
         h_off[i] = o;
         h_len[i] = l;
       }
       if (!l) continue;
-      r.lo = std::min(r.lo, o);
-      r.hi = std::max(r.hi, o + l);
-      r.sum += l;
-      const uint64_t g0 = (o - glo) >> gs, g1 = (o + l - 1 - glo) >> gs;
-      r.g0 = std::min(r.g0, g0);
-      r.g1 = std::max(r.g1, g1);
+      const uint64_t e = o + l;
+      lo = std::min(lo, o);
+      hi = std::max(hi, e);
+      sum += l;
+      // consecutive messages mostly share a granule (128 x 512 B per 64 KiB):
+      // mark a granule once per run, not once per message
+      const uint64_t g0 = (o - glo) >> gs, g1 = (e - 1 - glo) >> gs;
+      if (g0 == last && g1 == last) continue;
       for (uint64_t g = g0; g <= g1; ++g)
         if (!__atomic_load_n(&mark[g], __ATOMIC_RELAXED)) __atomic_store_n(&mark[g], 1, __ATOMIC_RELAXED);
+      last = g1;
     }
-    acc[t] = r;
+    ShardSpan& r = acc[t];
+    r.lo = lo;
+    r.hi = hi;
+    r.sum = sum;
   });
   ShardSpan sh;
   for (const ShardSpan& r : acc) {
     sh.lo = std::min(sh.lo, r.lo);
     sh.hi = std::max(sh.hi, r.hi);
     sh.sum += r.sum;
-    sh.g0 = std::min(sh.g0, r.g0);
-    sh.g1 = std::max(sh.g1, r.g1);
+  }
+  if (sh.any()) {  // the granules of the span's ends are the extreme marked ones
+    sh.g0 = (sh.lo - glo) >> gs;
+    sh.g1 = (sh.hi - 1 - glo) >> gs;
   }
   return sh;
+}
+
+ShardSpan stage_and_mark(const uint64_t* O, const uint64_t* L, uint64_t m, uint64_t glo, unsigned gs,
+                         uint64_t* h_off, uint64_t* h_len, std::vector<uint8_t>& mark) {
+  return h_off ? stage_and_mark_t<true>(O, L, m, glo, gs, h_off, h_len, mark)
+               : stage_and_mark_t<false>(O, L, m, glo, gs, h_off, h_len, mark);
 }
 
 // gmap[g] = device offset of granule gbase + g (marked granules packed back to
@@ -1493,21 +1509,34 @@ void scan_batch(const uint8_t* arena, uint64_t arena_len, const uint64_t* off, c
   parallel_chunks(P, T, [&](unsigned t, uint64_t p0, uint64_t p1) {
     Acc a;
     for (uint64_t p = p0; p < p1 && a.bad == UINT64_MAX; ++p) {
-      uint64_t blocks = 0;
-      for (uint64_t i = p * kPiece, e = std::min(n, (p + 1) * kPiece); i < e; ++i) {
+      // branch-free over the piece (the compiler vectorises it); a piece with a
+      // bad message is re-scanned for the first one
+      const uint64_t i0 = p * kPiece, i1 = std::min(n, (p + 1) * kPiece);
+      uint64_t blocks = 0, lo = a.lo, hi = a.hi, sum = a.sum, bits = a.offbits, bmax = a.bmax, bad = 0;
+      for (uint64_t i = i0; i < i1; ++i) {
         const uint64_t o = off[i], l = len[i];
-        if (l > arena_len || o > arena_len - l) {
-          a.bad = i;
-          break;
-        }
-        a.offbits |= o;
-        a.lo = std::min(a.lo, o);
-        a.hi = std::max(a.hi, o + l);
-        a.sum += l;
+        bad |= (uint64_t)(l > arena_len) | (uint64_t)(o > arena_len - l);
+        bits |= o;
+        lo = std::min(lo, o);
+        hi = std::max(hi, o + l);
+        sum += l;
         const uint64_t b = blocks_for(l);
         blocks += b;
-        a.bmax = std::max(a.bmax, b);
+        bmax = std::max(bmax, b);
       }
+      if (bad) {
+        for (uint64_t i = i0; i < i1; ++i)
+          if (len[i] > arena_len || off[i] > arena_len - len[i]) {
+            a.bad = i;
+            break;
+          }
+        break;
+      }
+      a.lo = lo;
+      a.hi = hi;
+      a.sum = sum;
+      a.offbits = bits;
+      a.bmax = bmax;
       r.csum[p + 1] = blocks;
     }
     acc[t] = a;
