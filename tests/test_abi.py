@@ -142,6 +142,26 @@ def test_create_error_travels_with_the_call_and_across_threads():
     assert lib.msha_ctx_create_err(mask, None, None, 0) == L.MSHA_ERR_INVALID_ARG
 
 
+def test_last_error_copy_truncates_and_reports_length():
+    """msha_last_error_copy copies the last error under a lock (ctx == NULL: the
+    last failed creation), NUL-terminates inside the buffer, never overruns it and
+    returns the full length; a NULL or empty buffer only reports the length."""
+    lib = L.lib()
+    ctx = ctypes.c_void_p()
+    n = ctypes.c_int(-1)
+    lib.msha_device_count(ctypes.byref(n))
+    mask = 1 << 31 if n.value > 0 else 1
+    full = ctypes.create_string_buffer(256)
+    assert lib.msha_ctx_create_err(mask, ctypes.byref(ctx), full, len(full)) == L.MSHA_ERR_NO_DEVICE
+    text = full.value
+    buf = ctypes.create_string_buffer(512)
+    assert lib.msha_last_error_copy(None, buf, len(buf)) == len(text) and buf.value == text
+    small = ctypes.create_string_buffer(b"\xff" * 8, 8)
+    assert lib.msha_last_error_copy(None, small, 4) == len(text)
+    assert small.raw[:3] == text[:3] and small.raw[3] == 0 and small.raw[4:] == b"\xff" * 4
+    assert lib.msha_last_error_copy(None, None, 0) == len(text)
+
+
 def test_stats_and_shard_stats_null_args():
     lib = L.lib()
     n = ctypes.c_uint32(0)
