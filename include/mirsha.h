@@ -223,7 +223,11 @@ int msha_set_kernel_policy(msha_ctx* ctx, int policy);
 /* Pinned host memory for callers that want zero-copy staging: when the arena
  * passed to msha_digest_batch lies in such memory, every message start is
  * 16-byte aligned and the messages are packed without large gaps, each GPU's
- * byte span of it is DMA'd as is (no gather copy into the library's staging). */
+ * byte span of it is DMA'd as is (no gather copy into the library's staging).
+ * On a context whose GPUs sit on several NUMA nodes the allocation is cut into
+ * one region per shard, in shard order, each placed on its GPU's node and
+ * page-locked with hipHostRegister (MSHA_PINNED_STRIPE=1 forces, =0 disables):
+ * a batch packed in message order then feeds each GPU from its own socket. */
 int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p);
 int msha_pinned_free(msha_ctx* ctx, void* p);
 

@@ -7,7 +7,12 @@
 // digests, join. There is no collective and no CPU hashing anywhere here.
 #include <hip/hip_runtime.h>
 
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <cctype>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -202,6 +207,7 @@ class WorkerPool {
 struct Device {
   int id = 0;
   uint32_t index = 0;  // shard number in the context
+  int numa = -1;       // NUMA node of the GPU's PCI device (-1: unknown)
   int cus = 256;
   hipStream_t stream = nullptr;       // kernels (and everything on single-stream paths)
   hipStream_t copy_stream = nullptr;  // H2D of staged chunks, overlapping the kernels
@@ -478,7 +484,9 @@ struct msha_ctx {
   std::vector<Device> devs;
   char err[512] = "";  // last failure on the context (fixed buffer: msha_last_error's pointer stays valid)
   msha_stats stats{};
-  std::vector<void*> pinned;  // allocations handed out by msha_pinned_alloc
+  // allocations handed out by msha_pinned_alloc: (pointer, mapped bytes), 0 =
+  // hipHostMalloc, else an mmap striped over NUMA nodes and hipHostRegister'ed
+  std::vector<std::pair<void*, uint64_t>> pinned;
   std::vector<uint64_t> tmp_len;
   int kernel_policy = MSHA_KERNEL_AUTO;
   // host planning buffers reused across calls
@@ -624,6 +632,79 @@ bool is_pinned_host(const void* p) {
     return false;
   }
   return a.type == hipMemoryTypeHost;
+}
+
+// NUMA node of GPU dev: its PCI device's numa_node in sysfs (-1: unknown).
+int gpu_numa_node(int dev) {
+  char bus[64] = {0};
+  if (hipDeviceGetPCIBusId(bus, sizeof bus, dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return -1;
+  }
+  for (char* c = bus; *c; ++c) *c = (char)std::tolower((unsigned char)*c);
+  char path[192];
+  std::snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bus);
+  FILE* f = std::fopen(path, "r");
+  if (!f) return -1;
+  int node = -1;
+  if (std::fscanf(f, "%d", &node) != 1) node = -1;
+  std::fclose(f);
+  return node;
+}
+
+// Does msha_pinned_alloc stripe its allocations over NUMA nodes? When the
+// context's GPUs sit on two or more nodes; MSHA_PINNED_STRIPE=1 forces it (a
+// one-node box exercises the path), =0 turns it off.
+bool stripe_pinned(const msha_ctx* ctx) {
+  if (const char* e = getenv("MSHA_PINNED_STRIPE")) return atoi(e) != 0;
+  for (const Device& d : ctx->devs)
+    if (d.numa >= 0 && d.numa != ctx->devs[0].numa) return true;
+  return false;
+}
+
+// A pinned allocation for a multi-socket context: cut into one region per shard,
+// in shard order, each preferring its shard's GPU's NUMA node (mbind), touched,
+// then page-locked for every GPU (hipHostRegister, portable). A caller that packs
+// a batch in message order (the Go adapter) then has each GPU's span -- shards
+// are contiguous message ranges -- mostly in its own socket's memory, instead of
+// every link reading one socket's. nullptr when a step fails (the caller then
+// takes hipHostMalloc); *mapped = the mapping's size.
+void* striped_pinned_alloc(const msha_ctx* ctx, uint64_t bytes, uint64_t* mapped) {
+  constexpr uint64_t kAlign = 2ull << 20;  // region edges on huge-page boundaries
+  const uint64_t size = (std::max<uint64_t>(bytes, 1) + kAlign - 1) & ~(kAlign - 1);
+  void* p = mmap(nullptr, size, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return nullptr;
+  const uint64_t k = ctx->devs.size();
+  for (uint64_t s = 0; s < k; ++s) {
+    const int node = ctx->devs[s].numa;
+    const uint64_t a = (size / k * s) & ~(kAlign - 1);
+    const uint64_t b = s + 1 == k ? size : (size / k * (s + 1)) & ~(kAlign - 1);
+    if (node < 0 || node >= 1024 || b <= a) continue;
+    unsigned long mask[1024 / (8 * sizeof(unsigned long))] = {0};
+    mask[node / (8 * sizeof(unsigned long))] |= 1ul << (node % (8 * sizeof(unsigned long)));
+    constexpr int kMpolPreferred = 1;  // <linux/mempolicy.h>; best effort: no error if refused
+    (void)syscall(SYS_mbind, static_cast<char*>(p) + a, b - a, kMpolPreferred, mask, 1024ul + 1, 0u);
+  }
+  // first touch places every page by its region's policy (several threads)
+  parallel_ranges(WorkerPool::get(), size / kAlign, size, [&](uint64_t a, uint64_t b) {
+    std::memset(static_cast<char*>(p) + a * kAlign, 0, (b - a) * kAlign);
+  });
+  if (hipHostRegister(p, size, hipHostRegisterPortable) != hipSuccess) {
+    (void)hipGetLastError();
+    munmap(p, size);
+    return nullptr;
+  }
+  *mapped = size;
+  return p;
+}
+
+void pinned_release(const std::pair<void*, uint64_t>& a) {
+  if (a.second) {
+    (void)hipHostUnregister(a.first);
+    munmap(a.first, a.second);
+  } else {
+    (void)hipHostFree(a.first);
+  }
 }
 
 inline uint32_t alias_tag(uint64_t off, uint64_t len) {
@@ -1857,6 +1938,7 @@ int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, i));
         d.cus = prop.multiProcessorCount;
+        d.numa = gpu_numa_node(i);
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
         HIPCHK(hipEventCreate(&d.ev0));
@@ -1898,7 +1980,7 @@ void msha_ctx_destroy(msha_ctx* ctx) {
     (void)hipStreamSynchronize(d.stream);
     d.release();
   }
-  for (void* p : ctx->pinned) (void)hipHostFree(p);
+  for (const auto& a : ctx->pinned) pinned_release(a);
   delete ctx;
 }
 
@@ -2045,21 +2127,53 @@ int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
     return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   if (action_part_begin[0] != 0 || action_part_begin[n_actions] != n_parts)
     return fail(ctx, MSHA_ERR_INVALID_ARG, "action_part_begin must start at 0 and end at n_parts");
-  for (uint64_t i = 0; i < n_actions; ++i)
-    if (action_part_begin[i + 1] < action_part_begin[i])
-      return fail(ctx, MSHA_ERR_INVALID_ARG, "action_part_begin must be non-decreasing");
-  for (uint64_t j = 0; j < n_parts; ++j)
-    if (part_len[j] > arena_len || part_off[j] > arena_len - part_len[j])
-      return fail(ctx, MSHA_ERR_INVALID_ARG, "part " + std::to_string(j) + " outside arena");
   const double t0 = now_ms();
   return guarded(ctx, [&] {
-    // Message length of each action = sum of its parts (h.Write appends).
+    // One threaded pass (2^18 parts and up) after the cheap monotonicity check:
+    // each thread validates the parts of its actions and sums their lengths
+    // (h.Write appends, so an action's message is its parts back to back). The
+    // error names the first bad part, as a serial scan would.
+    const unsigned T = plan_threads(std::max(n_actions, n_parts));
+    std::vector<uint64_t> bad(T, UINT64_MAX);
+    parallel_chunks(n_actions, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+      for (uint64_t i = lo; i < hi; ++i)
+        if (action_part_begin[i + 1] < action_part_begin[i]) {
+          bad[t] = i;
+          return;
+        }
+    });
+    for (uint64_t b : bad)
+      if (b != UINT64_MAX) throw MshaError(MSHA_ERR_INVALID_ARG, "action_part_begin must be non-decreasing");
     std::vector<uint64_t>& alen = ctx->tmp_len;
-    alen.assign(n_actions, 0);
-    uint64_t packed = 0;
-    for (uint64_t i = 0; i < n_actions; ++i) {
-      for (uint64_t j = action_part_begin[i]; j < action_part_begin[i + 1]; ++j) alen[i] += part_len[j];
-      packed += round16(alen[i]);
+    alen.resize(n_actions);
+    std::vector<uint64_t> packed_t(T, 0), bytes_t(T, 0), blocks_t(T, 0);
+    parallel_chunks(n_actions, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+      uint64_t packed = 0, bytes = 0, blocks = 0;
+      for (uint64_t i = lo; i < hi; ++i) {
+        uint64_t l = 0;
+        for (uint64_t j = action_part_begin[i]; j < action_part_begin[i + 1]; ++j) {
+          if (part_len[j] > arena_len || part_off[j] > arena_len - part_len[j]) {
+            bad[t] = j;
+            return;
+          }
+          l += part_len[j];
+        }
+        alen[i] = l;
+        packed += round16(l);
+        bytes += l;
+        blocks += blocks_for(l);
+      }
+      packed_t[t] = packed;
+      bytes_t[t] = bytes;
+      blocks_t[t] = blocks;
+    });
+    for (uint64_t b : bad)
+      if (b != UINT64_MAX) throw MshaError(MSHA_ERR_INVALID_ARG, "part " + std::to_string(b) + " outside arena");
+    uint64_t packed = 0, bytes = 0, blocks = 0;
+    for (unsigned t = 0; t < T; ++t) {
+      packed += packed_t[t];
+      bytes += bytes_t[t];
+      blocks += blocks_t[t];
     }
     auto gather = [&](uint64_t a, uint8_t* dst) {
       for (uint64_t j = action_part_begin[a]; j < action_part_begin[a + 1]; ++j) {
@@ -2071,8 +2185,6 @@ int msha_hash_actions(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len,
       run_small(ctx, t0, n_actions, alen.data(), out, gather);
     else
       run_pipeline(ctx, t0, n_actions, alen.data(), nullptr, out, gather);
-    uint64_t bytes = 0, blocks = 0;
-    for (uint64_t i = 0; i < n_actions; ++i) { bytes += alen[i]; blocks += blocks_for(alen[i]); }
     ctx->stats.messages += n_actions;
     ctx->stats.message_bytes += bytes;
     ctx->stats.blocks += blocks;
@@ -2092,9 +2204,18 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
     return fail(ctx, MSHA_ERR_INVALID_ARG, "begin must start at 0 and end at n_idx");
   for (uint64_t i = 0; i < n; ++i)
     if (begin[i + 1] < begin[i]) return fail(ctx, MSHA_ERR_INVALID_ARG, "begin must be non-decreasing");
-  for (uint64_t k = 0; k < n_idx; ++k)
-    if (idx[k] >= n_table) return fail(ctx, MSHA_ERR_INVALID_ARG, "idx out of table range");
   return guarded(ctx, [&] {
+    {  // threaded from 2^18 indices on
+      const unsigned T = plan_threads(n_idx);
+      std::vector<uint8_t> bad(T, 0);
+      parallel_chunks(n_idx, T, [&](unsigned t, uint64_t lo, uint64_t hi) {
+        uint32_t worst = 0;
+        for (uint64_t k = lo; k < hi; ++k) worst = std::max(worst, idx[k]);
+        bad[t] = hi > lo && worst >= n_table;
+      });
+      for (uint8_t b : bad)
+        if (b) throw MshaError(MSHA_ERR_INVALID_ARG, "idx out of table range");
+    }
     std::vector<uint64_t>& alen = ctx->tmp_len;
     alen.resize(n);
     uint64_t packed = 0;
@@ -2299,8 +2420,10 @@ int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p) {
 
   return guarded(ctx, [&] {
     HIPCHK(hipSetDevice(ctx->devs[0].id));
-    HIPCHK(hipHostMalloc(p, std::max<uint64_t>(bytes, 1), hipHostMallocPortable));
-    ctx->pinned.push_back(*p);
+    uint64_t mapped = 0;
+    *p = stripe_pinned(ctx) ? striped_pinned_alloc(ctx, bytes, &mapped) : nullptr;
+    if (!*p) HIPCHK(hipHostMalloc(p, std::max<uint64_t>(bytes, 1), hipHostMallocPortable));
+    ctx->pinned.emplace_back(*p, mapped);
   });
 }
 
@@ -2308,10 +2431,18 @@ int msha_pinned_free(msha_ctx* ctx, void* p) {
   if (!ctx) return MSHA_ERR_INVALID_ARG;
   std::lock_guard<std::mutex> lock(ctx->mu);
 
-  auto it = std::find(ctx->pinned.begin(), ctx->pinned.end(), p);
+  auto it = std::find_if(ctx->pinned.begin(), ctx->pinned.end(), [&](const auto& a) { return a.first == p; });
   if (it == ctx->pinned.end()) return fail(ctx, MSHA_ERR_INVALID_ARG, "pointer not from msha_pinned_alloc");
+  const std::pair<void*, uint64_t> a = *it;
   ctx->pinned.erase(it);
-  return guarded(ctx, [&] { HIPCHK(hipHostFree(p)); });
+  return guarded(ctx, [&] {
+    if (a.second) {
+      HIPCHK(hipHostUnregister(a.first));
+      munmap(a.first, a.second);
+    } else {
+      HIPCHK(hipHostFree(a.first));
+    }
+  });
 }
 
 }  // extern "C"

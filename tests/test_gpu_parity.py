@@ -185,6 +185,54 @@ def test_out_of_range_rejected(engine):
     assert ei.value.code == L.MSHA_ERR_INVALID_ARG
 
 
+@pytest.mark.parametrize("n_actions", [1000, 300_000])
+def test_hash_actions_rejects_first_bad_part(engine, n_actions):
+    """msha_hash_actions validates on several threads from 2^18 parts on: the
+    error still names the FIRST part outside the arena, a non-monotone
+    action_part_begin is rejected, and a valid batch of that size is bit-exact."""
+    rng = np.random.default_rng(n_actions)
+    per = rng.integers(0, 5, n_actions)
+    begin = np.concatenate([[0], np.cumsum(per)]).astype(np.uint64)
+    n_parts = int(begin[-1])
+    arena = W.random_bytes(W.SEED ^ 0x72, 0, 4096)
+    plen = rng.integers(0, 64, n_parts).astype(np.uint64)
+    poff = rng.integers(0, 4096 - 64, n_parts).astype(np.uint64)
+    got = engine.hash_actions_packed(arena, poff, plen, begin)
+    for a in rng.integers(0, n_actions, 64).tolist() + [0, n_actions - 1]:
+        msg = b"".join(arena[int(poff[j]):int(poff[j] + plen[j])].tobytes()
+                       for j in range(int(begin[a]), int(begin[a + 1])))
+        assert got[a].tobytes() == hashlib.sha256(msg).digest()
+    bad = poff.copy()
+    first, later = n_parts // 3, n_parts - 2
+    bad[later] = 4090
+    bad[first] = 4095
+    plen2 = plen.copy()
+    plen2[[first, later]] = 10
+    with pytest.raises(MshaError) as ei:
+        engine.hash_actions_packed(arena, bad, plen2, begin)
+    assert ei.value.code == L.MSHA_ERR_INVALID_ARG and f"part {first} outside arena" in str(ei.value)
+    b2 = begin.copy()
+    b2[n_actions // 2] = b2[n_actions // 2 + 1] + 1
+    with pytest.raises(MshaError) as ei:
+        engine.hash_actions_packed(arena, poff, plen, b2)
+    assert "non-decreasing" in str(ei.value)
+
+
+def test_digest_of_digests_rejects_index_past_table(engine):
+    """The index check of msha_digest_of_digests (threaded from 2^18 indices)."""
+    n = 20_000
+    table = W.random_bytes(W.SEED ^ 0x73, 0, 32 * 4096).reshape(4096, 32)
+    idx = np.random.default_rng(5).integers(0, 4096, 20 * n).astype(np.uint32)
+    begin = (np.arange(n + 1) * 20).astype(np.uint64)
+    idx[-1] = 4096
+    with pytest.raises(MshaError) as ei:
+        engine.digest_of_digests(table, idx, begin)
+    assert ei.value.code == L.MSHA_ERR_INVALID_ARG and "idx out of table range" in str(ei.value)
+    idx[-1] = 4095
+    out = engine.digest_of_digests(table, idx, begin)
+    assert out[-1].tobytes() == hashlib.sha256(table[idx[-20:]].tobytes()).digest()
+
+
 def test_empty_batch(engine):
     out = engine.digest_batch(np.zeros(0, dtype=np.uint8), np.zeros(0, dtype=np.uint64),
                               np.zeros(0, dtype=np.uint64))
@@ -571,6 +619,29 @@ def test_pinned_direct_gpu_planned(shards, monkeypatch):
             assert all(0 < s["upload_ms"] <= s["device_ms"] + 1e-3 and 0 < s["kernel_ms"] <= s["device_ms"] + 1e-3
                        for s in sh), sh
         assert e.stats()["direct_calls"] == 2
+
+
+def test_pinned_alloc_striped_over_numa_nodes(monkeypatch):
+    """msha_pinned_alloc on a context whose GPUs sit on several NUMA nodes cuts the
+    allocation into one region per shard, each bound to its GPU's node, and
+    page-locks it with hipHostRegister. MSHA_PINNED_STRIPE=1 forces that path on
+    this one-node box: the memory must still count as pinned (the direct path
+    runs), give bit-exact digests over 3 virtual shards, and free cleanly."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_PINNED_STRIPE", "1")
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", "3")
+    w = W.c5_storm(1 << 17)
+    exp = _oracle_dedup(w)
+    with Engine(1) as e:
+        arena = _pinned_copy(e, w.arena)
+        out = e.pinned_empty(w.n * 32).reshape(w.n, 32)
+        got = e.digest_batch(arena, _pinned_copy(e, w.off), _pinned_copy(e, w.len), out=out)
+        assert np.array_equal(got, exp)
+        assert e.stats()["direct_calls"] == 1
+        small = e.pinned_empty(100)                     # smaller than one 2 MiB region
+        small[:] = 7
+        assert e._lib.msha_pinned_free(e._ctx, small.ctypes.data) == 0
+        e._pinned.remove(small.ctypes.data)
 
 
 def _pinned_batch(e, lens, offs=None, seed=21):

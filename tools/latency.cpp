@@ -66,7 +66,7 @@ int main() {
     fprintf(stderr, "ctx: %s\n", err);
     return 1;
   }
-  const uint64_t kMaxN = 65536, kMsg = 512, kArena = kMaxN * kMsg + 64;
+  const uint64_t kMaxN = 262144, kMsg = 512, kArena = kMaxN * kMsg + 64;
   uint8_t* pinned = nullptr;
   uint8_t* pinned_out = nullptr;
   CHECK(msha_pinned_alloc(ctx, kArena, (void**)&pinned));
@@ -77,7 +77,7 @@ int main() {
   std::vector<uint64_t> off(kMaxN), len(kMaxN, kMsg);
   for (uint64_t i = 0; i < kMaxN; ++i) off[i] = kMsg * i;
 
-  const uint64_t sizes[] = {1, 4, 16, 64, 256, 1024, 4096, 16384, 65536};
+  const uint64_t sizes[] = {1, 4, 16, 64, 256, 1024, 4096, 16384, 65536, 262144};
   // request digests (clients.go:189-192): n x 512 B
   for (uint64_t n : sizes) {
     emit("msha_digest_batch", "pinned", n, n * kMsg, timed([&] {
