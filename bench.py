@@ -253,7 +253,7 @@ def host_api_leg(args, world: int) -> dict:
     return {"what": "c5 2^23 mixed actions, pinned arena -> msha_digest_batch -> pinned digests, one process, "
                     "one context over all the job's GPUs (PCIe-inclusive; NOT the headline)",
             "value": d["value"], "unit": "digests/s", "n_gpus": d["n_gpus"], "shards": d["shards"],
-            "virtual_shards": d["virtual_shards"], "ms_per_call": d["ms_per_step"],
+            "virtual_shards": d["virtual_shards"], "ms_per_call": d["ms_per_step"], "call_ms": d["call_ms"],
             "gbps_hashed": d["gbps_hashed"], "steps": d["steps"], "plan_ms": d["last_call_stats"]["plan_ms"],
             "first_launch_ms_max": max(x["first_launch_ms"] for x in d["last_call_shards"]),
             "per_gpu": [{k: x[k] for k in ("device", "messages", "lanes", "h2d_bytes", "device_ms", "upload_ms",
@@ -457,9 +457,12 @@ def run_lib(args):
         out = eng.pinned_empty(w.n * 32).reshape(w.n, 32)
     for _ in range(max(1, args.warmup)):
         eng.digest_batch(arena, off, ln, out=out)
+    calls = []
     t0 = time.perf_counter()
     for _ in range(args.steps):
+        t1 = time.perf_counter()
         eng.digest_batch(arena, off, ln, out=out)
+        calls.append((time.perf_counter() - t1) * 1e3)
     el = time.perf_counter() - t0
     st = eng.stats()
     sh = eng.shard_stats()
@@ -470,7 +473,8 @@ def run_lib(args):
         "value": w.n * args.steps / el, "unit": "digests/s", "n_gpus": n_gpus, "shards": shards,
         "virtual_shards": os.environ.get("MSHA_VIRTUAL_SHARDS"),
         "gbps_hashed": w.message_bytes * args.steps / el / 1e9, "steps": args.steps,
-        "ms_per_step": el / args.steps * 1e3, "config": {"workload": w.name, "config": args.config},
+        "ms_per_step": el / args.steps * 1e3, "call_ms": [round(c, 2) for c in calls],
+        "config": {"workload": w.name, "config": args.config},
         "scaling": "strong" if args.config == "c5" else "weak",
         "last_call_stats": st, "last_call_shards": sh}), flush=True)
     eng.close()

@@ -211,6 +211,8 @@ struct Device {
   int cus = 256;
   hipStream_t stream = nullptr;       // kernels (and everything on single-stream paths)
   hipStream_t copy_stream = nullptr;  // H2D of staged chunks, overlapping the kernels
+  hipStream_t d2h_stream = nullptr;   // host calls: digests back, behind their kernels (ev_k)
+  hipEvent_t ev_k = nullptr;          // the latest hash launch of a host call
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // device_ms / upload_ms / kernel_ms of the last host call: first H2D (copy
   // stream) .. last H2D, first hash kernel .. last kernel (msha_shard_stats)
@@ -263,7 +265,10 @@ struct Device {
     span_ev.clear();
     if (stream) (void)hipStreamDestroy(stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
-    stream = copy_stream = nullptr;
+    if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
+    if (ev_k) (void)hipEventDestroy(ev_k);
+    ev_k = nullptr;
+    stream = copy_stream = d2h_stream = nullptr;
   }
 };
 
@@ -1079,6 +1084,7 @@ void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_
   ctx->stats.h2d_bytes = h2d;
   ctx->stats.d2h_bytes = 32 + 32 * m;
   ctx->stats.total_ms = now_ms() - t0;
+  trace("done", t0);
 }
 
 // Launch shard d's lanes accumulated since its last launch, up to the end of
@@ -1089,6 +1095,20 @@ void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_
 // digests that are final: identity lanes' own slots, or (ordered lanes with
 // later_min) every slot below the lowest slot a later group writes -- into the
 // caller's buffer itself when it is pinned -- while later groups upload.
+// The stream a host call's digest D2H goes on: d2h_stream, ordered after
+// everything queued so far on `after` (its kernels). On the kernel stream itself
+// a D2H would hold up the next launch for as long as the copy takes, and on a
+// box whose PCIe writes are slowed by other traffic that delayed c5's last
+// kernels by up to 9 ms. MSHA_D2H_STREAM=0 keeps the D2H on the kernel stream
+// (A/B, tools/ab_d2h.sh).
+hipStream_t d2h_stream_after(Device& d, hipStream_t after) {
+  const bool own = env_u64("MSHA_D2H_STREAM", 1) != 0;
+  if (!own) return after;
+  HIPCHK(hipEventRecord(d.ev_k, after));
+  HIPCHK(hipStreamWaitEvent(d.d2h_stream, d.ev_k, 0));
+  return d.d2h_stream;
+}
+
 void launch_lanes(msha_ctx* ctx, Device& d, Plan& P, size_t c, bool last, double t0, uint8_t* out,
                   bool out_pinned) {
   const uint64_t q1 = P.lane_cut[c + 1];
@@ -1112,16 +1132,17 @@ void launch_lanes(msha_ctx* ctx, Device& d, Plan& P, size_t c, bool last, double
       ctx->kernel_policy, d.stream, split_for(d, lanes, ctx->kernel_policy, sp), &kind));
   count_launch(ctx, &d, kind);
   uint8_t* dst = out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>();
+  const bool d2h = P.identity() || (!P.later_min.empty() && P.later_min[c + 1] > P.d2h_done);
+  hipStream_t ds = d2h ? d2h_stream_after(d, d.stream) : d.stream;
   if (P.identity()) {
-    HIPCHK(hipMemcpyAsync(dst + 32 * l0, d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost,
-                          d.stream));
+    HIPCHK(hipMemcpyAsync(dst + 32 * l0, d.out.as<uint8_t>() + 32 * l0, 32 * lanes, hipMemcpyDeviceToHost, ds));
     d.st.d2h_bytes += 32 * lanes;
   } else if (!P.later_min.empty()) {
     // aliases among the streamed slots are filled on the host after the sync
     const uint64_t x = P.later_min[c + 1];
     if (x > P.d2h_done) {
       HIPCHK(hipMemcpyAsync(dst + 32 * P.d2h_done, d.out.as<uint8_t>() + 32 * P.d2h_done, 32 * (x - P.d2h_done),
-                            hipMemcpyDeviceToHost, d.stream));
+                            hipMemcpyDeviceToHost, ds));
       d.st.d2h_bytes += 32 * (x - P.d2h_done);
       P.d2h_done = x;
     }
@@ -1135,15 +1156,16 @@ void queue_tail(Device& d, Plan& P, uint8_t* out, bool out_pinned) {
   if (m == 0) return;
   HIPCHK(hipSetDevice(d.id));
   HIPCHK(hipEventRecord(d.ev1, d.stream));
+  const hipStream_t ds = d2h_stream_after(d, d.stream);
   const uint64_t done = P.d2h_done;  // slots streamed back after earlier launches
   if (!P.identity() && done < m) {
     // d.out is message-ordered (lane q wrote its message's slot); a pinned result
     // buffer takes it as is, the aliases' slots are filled on the host afterwards
     HIPCHK(hipMemcpyAsync((out_pinned ? out + 32 * d.lo : d.h_out.as<uint8_t>()) + 32 * done,
-                          d.out.as<uint8_t>() + 32 * done, 32 * (m - done), hipMemcpyDeviceToHost, d.stream));
+                          d.out.as<uint8_t>() + 32 * done, 32 * (m - done), hipMemcpyDeviceToHost, ds));
     d.st.d2h_bytes += 32 * (m - done);
   }
-  HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, d.stream));
+  HIPCHK(hipMemcpyAsync(d.h_out.as<uint8_t>() + 32 * m, d.err.p, 4, hipMemcpyDeviceToHost, ds));
   d.st.d2h_bytes += 4;
 }
 
@@ -1159,16 +1181,20 @@ float elapsed_ms(hipEvent_t a, hipEvent_t b) {
 // timed out, fill its aliases' digests (each copies its representative's) and
 // complete its msha_shard_stats: device_ms = first upload .. last kernel,
 // upload_ms = first .. last upload, kernel_ms = first kernel .. last (HIP events).
-void finish_shard(msha_ctx* ctx, uint32_t s, uint8_t* out, bool out_pinned) {
+void finish_shard(msha_ctx* ctx, uint32_t s, uint8_t* out, bool out_pinned, double t0) {
   Device& d = ctx->devs[s];
   Plan& P = ctx->plans[s];
   const uint64_t m = P.m;
   if (m == 0) return;
   HIPCHK(hipSetDevice(d.id));
   HIPCHK(hipStreamSynchronize(d.stream));
+  HIPCHK(hipStreamSynchronize(d.d2h_stream));
   d.st.device_ms = elapsed_ms(d.ev_up0, d.ev1);
   d.st.upload_ms = elapsed_ms(d.ev_up0, d.ev_up1);
   d.st.kernel_ms = elapsed_ms(d.ev_k0, d.ev1);
+  if (trace_on())
+    fprintf(stderr, "[msha] shard %u %-16s %9.2f ms (device %.2f, upload %.2f, kernels %.2f ms)\n", s, "synced",
+            now_ms() - t0, d.st.device_ms, d.st.upload_ms, d.st.kernel_ms);
   uint32_t errflag;
   std::memcpy(&errflag, d.h_out.as<uint8_t>() + 32 * m, 4);
   const bool straight = out_pinned;  // the digests were D2H'd straight into out
@@ -1463,7 +1489,7 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
   }
   for_each_shard(ctx, [&](uint32_t s) {
     queue_tail(ctx->devs[s], plans[s], out, out_pinned);
-    finish_shard(ctx, s, out, out_pinned);
+    finish_shard(ctx, s, out, out_pinned, t0);
   });
   call_stats(ctx, t0, t_plan);
 }
@@ -1677,14 +1703,42 @@ struct Arrival {
   }
 };
 
+// Pinned off/len of a one-shard call: uploaded to the shard's p_meta as the
+// call starts, before validation, which the link would otherwise sit idle for
+// (c5 on one GPU: 1.3 ms of a 72 ms call). Only the direct path consumes the
+// upload; on any other path (or an error) the destructor drains it, so off/len
+// are no longer read once the call returns.
+struct EarlyMeta {
+  Device* d = nullptr;
+  bool used = false;
+  EarlyMeta(msha_ctx* ctx, const uint64_t* off, const uint64_t* len, uint64_t n) {
+    if (ctx->devs.size() != 1 || n <= small_msgs()) return;
+    if (!(is_pinned_host(off) && is_pinned_host(off + n - 1) && is_pinned_host(len) && is_pinned_host(len + n - 1)))
+      return;
+    Device& dv = ctx->devs[0];
+    HIPCHK(hipSetDevice(dv.id));
+    dv.p_meta.ensure(16 * n);
+    HIPCHK(hipEventRecord(dv.ev_up0, dv.copy_stream));
+    HIPCHK(hipMemcpyAsync(dv.p_meta.p, off, 8 * n, hipMemcpyHostToDevice, dv.copy_stream));
+    HIPCHK(hipMemcpyAsync(dv.p_meta.as<uint64_t>() + n, len, 8 * n, hipMemcpyHostToDevice, dv.copy_stream));
+    d = &dv;
+  }
+  bool queued() const { return d != nullptr; }
+  ~EarlyMeta() {
+    if (d && !used) (void)hipStreamSynchronize(d->copy_stream);
+  }
+};
+
 void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const uint64_t* len,
-                const uint8_t* arena, uint8_t* out, const BatchScan& sc) {
+                const uint8_t* arena, uint8_t* out, const BatchScan& sc, EarlyMeta* early = nullptr) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   const bool out_pinned = is_pinned_host(out) && is_pinned_host(out + 32 * n - 1);
   // off/len in pinned memory (msha_pinned_alloc, as the Go adapter packs them):
-  // uploaded as they are, no staging copy
-  const bool meta_pinned = is_pinned_host(off) && is_pinned_host(off + n - 1) && is_pinned_host(len) &&
-                           is_pinned_host(len + n - 1);
+  // uploaded as they are, no staging copy (one shard: already on the way, EarlyMeta)
+  const bool meta_early = early && early->queued();
+  if (meta_early) early->used = true;
+  const bool meta_pinned = meta_early || (is_pinned_host(off) && is_pinned_host(off + n - 1) &&
+                                          is_pinned_host(len) && is_pinned_host(len + n - 1));
   std::vector<uint64_t> bounds(k + 1);
   if (k == 1) {
     bounds[0] = 0;
@@ -1733,7 +1787,7 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
     // Pinned off/len go up right away, under the marking pass (c5 on one GPU:
     // 134 MB, ~2.5 ms of PCIe that no longer waits for the host).
     d.p_meta.ensure(16 * m);
-    if (meta_pinned) {
+    if (meta_pinned && !meta_early) {
       HIPCHK(hipEventRecord(d.ev_up0, d.copy_stream));
       HIPCHK(hipMemcpyAsync(d.p_meta.p, O, 8 * m, hipMemcpyHostToDevice, d.copy_stream));
       HIPCHK(hipMemcpyAsync(d.p_meta.as<uint64_t>() + m, L, 8 * m, hipMemcpyHostToDevice, d.copy_stream));
@@ -1876,7 +1930,7 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
       launch_lanes(ctx, d, P, g, g + 1 == groups, t0, out, out_pinned);
     }
     queue_tail(d, P, out, out_pinned);
-    finish_shard(ctx, s, out, out_pinned);
+    finish_shard(ctx, s, out, out_pinned, t0);
   });
   double t_plan = t0;  // plan_ms: until the last shard's first kernel is queued
   for (const Device& d : ctx->devs) t_plan = std::max(t_plan, t0 + d.st.first_launch_ms);
@@ -1941,6 +1995,8 @@ int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint
         d.numa = gpu_numa_node(i);
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
+        HIPCHK(hipStreamCreateWithFlags(&d.d2h_stream, hipStreamNonBlocking));
+        HIPCHK(hipEventCreateWithFlags(&d.ev_k, hipEventDisableTiming));
         HIPCHK(hipEventCreate(&d.ev0));
         HIPCHK(hipEventCreate(&d.ev1));
         HIPCHK(hipEventCreate(&d.ev_up0));
@@ -1977,7 +2033,8 @@ void msha_ctx_destroy(msha_ctx* ctx) {
   if (!ctx) return;
   for (auto& d : ctx->devs) {
     (void)hipSetDevice(d.id);
-    (void)hipStreamSynchronize(d.stream);
+    for (hipStream_t st : {d.stream, d.copy_stream, d.d2h_stream})
+      if (st) (void)hipStreamSynchronize(st);
     d.release();
   }
   for (const auto& a : ctx->pinned) pinned_release(a);
@@ -2063,6 +2120,7 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
   if (n >= 0xffffffffull) return fail(ctx, MSHA_ERR_INVALID_ARG, "more than 2^32-2 messages in one call");
   const double t0 = now_ms();
   return guarded(ctx, [&] {
+    EarlyMeta early(ctx, off, len, n);
     BatchScan sc;
     scan_batch(arena, arena_len, off, len, n, sc);
     const uint64_t lo = sc.lo, hi = sc.hi, sum = sc.sum;
@@ -2097,7 +2155,7 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
     const bool direct = aligned16 && hi > lo && hi - lo <= std::min(sum, hi - lo) + 16 * n + (1u << 20) &&
                         is_pinned_host(arena + lo) && is_pinned_host(arena + hi - 1);
     if (direct) {
-      run_direct(ctx, t0, n, off, len, arena, out, sc);
+      run_direct(ctx, t0, n, off, len, arena, out, sc, &early);
       ctx->stats.direct_calls++;
       count();
       return;

@@ -644,6 +644,32 @@ def test_pinned_alloc_striped_over_numa_nodes(monkeypatch):
         e._pinned.remove(small.ctypes.data)
 
 
+def test_early_metadata_upload_on_every_path():
+    """Pinned off/len of a one-shard call go up before validation (EarlyMeta);
+    only the direct path consumes that upload. With a pageable arena (the
+    pipeline path), an unaligned pinned arena, and a batch that fails validation,
+    the call must still be bit-exact or fail cleanly, and the next direct call
+    correct."""
+    from mirbft_amd import Engine
+    w = W.c2_requests(n=100_000)
+    exp = oracle.digest_batch(w.arena, w.off, w.len)
+    with Engine(1) as e:
+        off, ln = _pinned_copy(e, w.off), _pinned_copy(e, w.len)
+        assert np.array_equal(e.digest_batch(w.arena, off, ln), exp)          # pageable arena
+        parena = _pinned_copy(e, w.arena)
+        shifted = e.pinned_empty(w.arena.size + 1)
+        shifted[1:] = w.arena
+        off1 = _pinned_copy(e, w.off + np.uint64(1))
+        assert np.array_equal(e.digest_batch(shifted, off1, ln), exp)         # unaligned: not direct
+        bad = _pinned_copy(e, w.off)
+        bad[-1] = w.arena.size                                               # outside the arena
+        with pytest.raises(MshaError):
+            e.digest_batch(parena, bad, ln)
+        before = e.stats()["direct_calls"]
+        assert np.array_equal(e.digest_batch(parena, off, ln), exp)          # direct, early metadata
+        assert e.stats()["direct_calls"] == before + 1
+
+
 def _pinned_batch(e, lens, offs=None, seed=21):
     """A pinned arena holding messages of the given lengths (16-byte aligned starts
     unless offs is given) and the oracle's digests."""
