@@ -211,7 +211,8 @@ struct Device {
   int cus = 256;
   hipStream_t stream = nullptr;       // kernels (and everything on single-stream paths)
   hipStream_t copy_stream = nullptr;  // H2D of staged chunks, overlapping the kernels
-  hipStream_t d2h_stream = nullptr;   // host calls: digests back, behind their kernels (ev_k)
+  hipStream_t d2h_stream = nullptr;   // host calls: digests back, behind their kernels (ev_k);
+                                      // only on a GPU no other shard shares (d2h_stream_after)
   hipEvent_t ev_k = nullptr;          // the latest hash launch of a host call
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // device_ms / upload_ms / kernel_ms of the last host call: first H2D (copy
@@ -1100,10 +1101,12 @@ void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_
 // a D2H would hold up the next launch for as long as the copy takes, and on a
 // box whose PCIe writes are slowed by other traffic that delayed c5's last
 // kernels by up to 9 ms. MSHA_D2H_STREAM=0 keeps the D2H on the kernel stream
-// (A/B, tools/ab_d2h.sh).
+// (A/B, tools/ab_d2h.py). Shards sharing one GPU (MSHA_VIRTUAL_SHARDS) keep it
+// on the kernel stream: HIP multiplexes streams over GPU_MAX_HW_QUEUES (4)
+// hardware queues per device, and a third stream per shard put D2H waits in
+// front of other shards' uploads (c5 at 2 virtual shards 71.5 -> 89 ms per call).
 hipStream_t d2h_stream_after(Device& d, hipStream_t after) {
-  const bool own = env_u64("MSHA_D2H_STREAM", 1) != 0;
-  if (!own) return after;
+  if (!d.d2h_stream || env_u64("MSHA_D2H_STREAM", 1) == 0) return after;
   HIPCHK(hipEventRecord(d.ev_k, after));
   HIPCHK(hipStreamWaitEvent(d.d2h_stream, d.ev_k, 0));
   return d.d2h_stream;
@@ -1188,7 +1191,7 @@ void finish_shard(msha_ctx* ctx, uint32_t s, uint8_t* out, bool out_pinned, doub
   if (m == 0) return;
   HIPCHK(hipSetDevice(d.id));
   HIPCHK(hipStreamSynchronize(d.stream));
-  HIPCHK(hipStreamSynchronize(d.d2h_stream));
+  if (d.d2h_stream) HIPCHK(hipStreamSynchronize(d.d2h_stream));
   d.st.device_ms = elapsed_ms(d.ev_up0, d.ev1);
   d.st.upload_ms = elapsed_ms(d.ev_up0, d.ev_up1);
   d.st.kernel_ms = elapsed_ms(d.ev_k0, d.ev1);
@@ -1995,8 +1998,10 @@ int msha_ctx_create_err(uint32_t device_mask, msha_ctx** out, char* errbuf, uint
         d.numa = gpu_numa_node(i);
         HIPCHK(hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking));
         HIPCHK(hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
-        HIPCHK(hipStreamCreateWithFlags(&d.d2h_stream, hipStreamNonBlocking));
-        HIPCHK(hipEventCreateWithFlags(&d.ev_k, hipEventDisableTiming));
+        if (virt == 1) {
+          HIPCHK(hipStreamCreateWithFlags(&d.d2h_stream, hipStreamNonBlocking));
+          HIPCHK(hipEventCreateWithFlags(&d.ev_k, hipEventDisableTiming));
+        }
         HIPCHK(hipEventCreate(&d.ev0));
         HIPCHK(hipEventCreate(&d.ev1));
         HIPCHK(hipEventCreate(&d.ev_up0));
