@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 5u
+#define MSHA_ABI_VERSION 6u
 
 enum {
   MSHA_OK = 0,
@@ -88,6 +88,9 @@ typedef struct {
   uint64_t h2d_bytes;       /* payload + metadata uploaded */
   uint64_t d2h_bytes;       /* digests + status words downloaded */
   uint64_t small_calls;     /* host calls served by the small-call (latency) path: one H2D, one launch, one D2H */
+  uint64_t staged_calls;    /* host calls whose pageable arena had the direct path's shape (16-B aligned,
+                               dense): its touched runs went up through pinned staging, lanes planned
+                               on the GPU (ABI 6) */
 } msha_stats;
 
 /* Per-GPU figures of the last host-memory call (one entry per shard; a shard is

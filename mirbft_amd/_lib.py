@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -53,6 +53,7 @@ class MshaStats(ctypes.Structure):
         ("h2d_bytes", ctypes.c_uint64),
         ("d2h_bytes", ctypes.c_uint64),
         ("small_calls", ctypes.c_uint64),
+        ("staged_calls", ctypes.c_uint64),
     ]
 
 

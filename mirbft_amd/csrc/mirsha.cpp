@@ -1706,6 +1706,31 @@ struct Arrival {
   }
 };
 
+// Has event e completed? (A not-ready query leaves no error behind for a later
+// hipGetLastError to pick up.)
+bool event_done(hipEvent_t e) {
+  const hipError_t r = hipEventQuery(e);
+  if (r == hipSuccess) return true;
+  (void)hipGetLastError();
+  if (r != hipErrorNotReady) HIPCHK(r);
+  return false;
+}
+
+// memcpy of a large contiguous range on the calling thread's pool (>= 2 MiB a thread).
+void copy_threads(uint8_t* dst, const uint8_t* src, uint64_t bytes) {
+  WorkerPool& pool = cur_pool();
+  const unsigned T = (unsigned)std::min<uint64_t>(pool.size(), std::max<uint64_t>(1, bytes >> 21));
+  if (T <= 1) {
+    std::memcpy(dst, src, bytes);
+    return;
+  }
+  const std::function<void(unsigned)> job = [&](unsigned t) {
+    const uint64_t a = (bytes * t / T) & ~uint64_t(63), b = t + 1 == T ? bytes : (bytes * (t + 1) / T) & ~uint64_t(63);
+    std::memcpy(dst + a, src + a, b - a);
+  };
+  pool.run(T, job);
+}
+
 // Pinned off/len of a one-shard call: uploaded to the shard's p_meta as the
 // call starts, before validation, which the link would otherwise sit idle for
 // (c5 on one GPU: 1.3 ms of a 72 ms call). Only the direct path consumes the
@@ -1733,7 +1758,7 @@ struct EarlyMeta {
 };
 
 void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const uint64_t* len,
-                const uint8_t* arena, uint8_t* out, const BatchScan& sc, EarlyMeta* early = nullptr) {
+                const uint8_t* arena, uint8_t* out, const BatchScan& sc, EarlyMeta* early, bool staged) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   const bool out_pinned = is_pinned_host(out) && is_pinned_host(out + 32 * n - 1);
   // off/len in pinned memory (msha_pinned_alloc, as the Go adapter packs them):
@@ -1891,47 +1916,93 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
     for (uint32_t o = 0; shared_gpu && o < k; ++o)
       if (o != s && meta_queued[o] && ctx->devs[o].id == d.id)
         HIPCHK(hipStreamWaitEvent(d.copy_stream, ctx->devs[o].ev_meta, 0));
+    // 5. the plan's lane groups (read back once the planner is done), each
+    // launched behind the upload piece that completes its payloads
+    bool planned = false;
+    size_t groups = 0, next_group = 0;
+    auto read_plan = [&] {
+      d.st.plan_kernel_ms = elapsed_ms(d.ev_p0, d.ev_p1);
+      const uint32_t* gmin = d.h_small.as<uint32_t>();
+      const uint32_t* cut = gmin + chunks;
+      P.lanes = cut[chunks];
+      d.st.lanes = P.lanes;
+      P.rep_dev = aliases ? d.h_rep.as<uint32_t>() : nullptr;
+      // lane groups: one per piece that completes at least one payload
+      P.lane_cut.assign(1, 0);
+      P.cut_chunk.clear();
+      std::vector<uint64_t> gm;
+      for (uint64_t q = 0; q < chunks; ++q) {
+        if (cut[q + 1] == cut[q]) continue;
+        P.lane_cut.push_back(cut[q + 1]);
+        P.cut_chunk.push_back(q);
+        gm.push_back(gmin[q]);
+      }
+      groups = gm.size();
+      P.later_min.assign(groups + 1, m);
+      for (size_t g = groups; g-- > 0;) P.later_min[g] = std::min<uint64_t>(gm[g], P.later_min[g + 1]);
+      planned = true;
+      trace("planned on GPU", s, t0);
+    };
+    auto launch_upto = [&](uint64_t pieces_queued) {  // pieces [0, pieces_queued) have their events
+      for (; next_group < groups && P.cut_chunk[next_group] < pieces_queued; ++next_group) {
+        HIPCHK(hipStreamWaitEvent(d.stream, d.span_ev[P.cut_chunk[next_group]], 0));
+        launch_lanes(ctx, d, P, next_group, next_group + 1 == groups, t0, out, out_pinned);
+      }
+    };
     // event c once every byte below device offset (c+1)*kDirectChunk is queued
     uint64_t c = 0, uploaded = 0;
+    auto pieces_done = [&](uint64_t dev_end) {
+      for (; c < chunks && (c + 1) * kDirectChunk <= dev_end; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+    };
+    unsigned slot_i = 0;
+    if (staged) {  // two pinned staging slots, refilled as their H2D drains
+      d.slot[0].ensure(kChunkBytes);
+      d.slot[1].ensure(kChunkBytes);
+      HIPCHK(hipEventRecord(d.slot_free[0], d.copy_stream));
+      HIPCHK(hipEventRecord(d.slot_free[1], d.copy_stream));
+    }
     if (any)
       for_each_upload(gmap, ng, gbase, glo, gs, sh.lo, sh.hi, [&](uint64_t pos, uint64_t dev, uint64_t bytes) {
-        HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + dev, arena + pos, bytes, hipMemcpyHostToDevice,
-                              d.copy_stream));
-        uploaded += bytes;
-        for (; c < chunks && (c + 1) * kDirectChunk <= dev + bytes; ++c)
-          HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+        if (!staged) {  // the caller's pinned bytes, DMA'd as they are
+          HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + dev, arena + pos, bytes, hipMemcpyHostToDevice,
+                                d.copy_stream));
+          uploaded += bytes;
+          pieces_done(dev + bytes);
+          return;
+        }
+        // pageable: copied into a staging slot by the shard's threads (large
+        // contiguous runs, not message by message), then DMA'd; kernels start
+        // as their pieces land and the planner's result is in
+        for (uint64_t o = 0; o < bytes;) {
+          const uint64_t take = std::min(bytes - o, kChunkBytes);
+          const unsigned si = slot_i++ & 1;
+          HIPCHK(hipEventSynchronize(d.slot_free[si]));
+          const double g0 = now_ms();
+          copy_threads(d.slot[si].as<uint8_t>(), arena + pos + o, take);
+          const double g1 = now_ms();
+          if (d.st.gather_begin_ms == 0) d.st.gather_begin_ms = std::max(g0 - t0, 1e-6);
+          d.st.gather_end_ms = g1 - t0;
+          d.st.gather_ms += g1 - g0;
+          HIPCHK(hipMemcpyAsync(d.arena.as<uint8_t>() + dev + o, d.slot[si].p, take, hipMemcpyHostToDevice,
+                                d.copy_stream));
+          HIPCHK(hipEventRecord(d.slot_free[si], d.copy_stream));
+          o += take;
+          uploaded += take;
+          pieces_done(dev + o);
+          if (!planned && event_done(d.ev_plan)) read_plan();
+          if (planned) launch_upto(c);
+        }
       });
     for (; c < chunks; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
     HIPCHK(hipEventRecord(d.ev_up1, d.copy_stream));
     d.st.h2d_payload_bytes = uploaded;
     d.st.h2d_bytes = 16 * m + 8 * ng;
     trace("payload queued", s, t0);
-    HIPCHK(hipEventSynchronize(d.ev_plan));
-    d.st.plan_kernel_ms = elapsed_ms(d.ev_p0, d.ev_p1);
-    const uint32_t* gmin = d.h_small.as<uint32_t>();
-    const uint32_t* cut = gmin + chunks;
-    P.lanes = cut[chunks];
-    d.st.lanes = P.lanes;
-    P.rep_dev = aliases ? d.h_rep.as<uint32_t>() : nullptr;
-    // lane groups: one per piece that completes at least one payload
-    P.lane_cut.assign(1, 0);
-    P.cut_chunk.clear();
-    std::vector<uint64_t> gm;
-    for (uint64_t q = 0; q < chunks; ++q) {
-      if (cut[q + 1] == cut[q]) continue;
-      P.lane_cut.push_back(cut[q + 1]);
-      P.cut_chunk.push_back(q);
-      gm.push_back(gmin[q]);
+    if (!planned) {
+      HIPCHK(hipEventSynchronize(d.ev_plan));
+      read_plan();
     }
-    const size_t groups = gm.size();
-    P.later_min.assign(groups + 1, m);
-    for (size_t g = groups; g-- > 0;) P.later_min[g] = std::min<uint64_t>(gm[g], P.later_min[g + 1]);
-    trace("planned on GPU", s, t0);
-    // 5. one launch per accumulated lane group, each behind its piece's upload
-    for (size_t g = 0; g < groups; ++g) {
-      HIPCHK(hipStreamWaitEvent(d.stream, d.span_ev[P.cut_chunk[g]], 0));
-      launch_lanes(ctx, d, P, g, g + 1 == groups, t0, out, out_pinned);
-    }
+    launch_upto(chunks);
     queue_tail(d, P, out, out_pinned);
     finish_shard(ctx, s, out, out_pinned, t0);
   });
@@ -2157,11 +2228,14 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
     // Zero-copy upload when the caller packed into pinned memory (msha_pinned_alloc)
     // with 16-byte aligned message starts and little waste between messages:
     // the touched byte ranges go up as they are and the GPU plans the lanes.
-    const bool direct = aligned16 && hi > lo && hi - lo <= std::min(sum, hi - lo) + 16 * n + (1u << 20) &&
-                        is_pinned_host(arena + lo) && is_pinned_host(arena + hi - 1);
-    if (direct) {
-      run_direct(ctx, t0, n, off, len, arena, out, sc, &early);
-      ctx->stats.direct_calls++;
+    // A pageable arena of the same shape takes the same path, its touched runs
+    // copied through pinned staging slots (staged_calls; MSHA_STAGED_DIRECT=0:
+    // the gather pipeline below instead).
+    const bool dense = aligned16 && hi > lo && hi - lo <= std::min(sum, hi - lo) + 16 * n + (1u << 20);
+    const bool pinned = dense && is_pinned_host(arena + lo) && is_pinned_host(arena + hi - 1);
+    if (pinned || (dense && env_u64("MSHA_STAGED_DIRECT", 1) != 0)) {
+      run_direct(ctx, t0, n, off, len, arena, out, sc, &early, !pinned);
+      (pinned ? ctx->stats.direct_calls : ctx->stats.staged_calls)++;
       count();
       return;
     }

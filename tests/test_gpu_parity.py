@@ -432,12 +432,15 @@ def test_c5_device_ordered(engine):
     assert np.array_equal(out.cpu().numpy(), oracle.digest_batch(w.arena, w.off, w.len))
 
 
+@pytest.mark.parametrize("staged", ["1", "0"])
 @pytest.mark.parametrize("shards", [2, 3])
-def test_host_path_sharded(shards, monkeypatch):
+def test_host_path_sharded(shards, staged, monkeypatch):
     """The multi-GPU host path (partition by blocks, per-shard placement, alias
-    dedup reset per shard, per-shard order) on virtual shards of one GPU."""
+    dedup reset per shard, per-shard order) on virtual shards of one GPU: the
+    staged direct path, and the gather pipeline (MSHA_STAGED_DIRECT=0)."""
     from mirbft_amd import Engine
     monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", str(shards))
+    monkeypatch.setenv("MSHA_STAGED_DIRECT", staged)
     with Engine(1) as e:
         w = W.c5_storm(1 << 15)                      # aliased EpochChange pool + mixed sizes
         assert np.array_equal(e.digest_batch(w.arena, w.off, w.len),
@@ -492,9 +495,11 @@ def test_pinned_arena_direct_upload(engine):
     off2 += 8
     assert np.array_equal(engine.digest_batch(pinned2, off2, w.len), exp)
     assert engine.stats()["direct_calls"] == before + 1
-    # pageable memory: gather path
+    # pageable memory of the same shape: the same GPU-planned path, staged
+    staged = engine.stats()["staged_calls"]
     assert np.array_equal(engine.digest_batch(w.arena, w.off, w.len), exp)
     assert engine.stats()["direct_calls"] == before + 1
+    assert engine.stats()["staged_calls"] == staged + 1
 
 
 def _oracle_dedup(w):
@@ -668,6 +673,36 @@ def test_early_metadata_upload_on_every_path():
         before = e.stats()["direct_calls"]
         assert np.array_equal(e.digest_batch(parena, off, ln), exp)          # direct, early metadata
         assert e.stats()["direct_calls"] == before + 1
+
+
+@pytest.mark.parametrize("shards", [1, 3])
+def test_staged_direct_pageable(shards, monkeypatch):
+    """A pageable arena of the direct path's shape (16-B aligned, dense) is planned
+    on the GPU like a pinned one, its touched runs copied through two pinned
+    staging slots while earlier ones upload and their lane groups hash: c5
+    batches (aliases folded on the GPU) with pageable or pinned off/len and
+    pageable or pinned digests, bit-exact, staged_calls counted, the copy timed;
+    with MSHA_STAGED_DIRECT=0 the same batch takes the gather pipeline."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", str(shards))
+    w = W.c5_storm(3 << 17)
+    exp = _oracle_dedup(w)
+    with Engine(1) as e:
+        for meta, outk in (("pageable", "pageable"), ("pinned", "pinned")):
+            off, ln = (w.off, w.len) if meta == "pageable" else (_pinned_copy(e, w.off), _pinned_copy(e, w.len))
+            out = None if outk == "pageable" else e.pinned_empty(w.n * 32).reshape(w.n, 32)
+            st0 = e.stats()
+            got = e.digest_batch(w.arena, off, ln, out=out)
+            assert np.array_equal(got, exp), (meta, outk)
+            st1 = e.stats()
+            assert st1["staged_calls"] == st0["staged_calls"] + 1 and st1["direct_calls"] == st0["direct_calls"]
+            sh = e.shard_stats()
+            assert sum(s["lanes"] for s in sh) < w.n
+            assert all(s["gather_ms"] > 0 and s["first_launch_ms"] > 0 for s in sh), sh
+        monkeypatch.setenv("MSHA_STAGED_DIRECT", "0")
+        st0 = e.stats()
+        assert np.array_equal(e.digest_batch(w.arena, w.off, w.len), exp)
+        assert e.stats()["staged_calls"] == st0["staged_calls"]
 
 
 def _pinned_batch(e, lens, offs=None, seed=21):
@@ -896,12 +931,15 @@ def test_direct_upload_compacted_ranges_sharded(monkeypatch):
         assert sum(s["messages"] for s in sh) == w.n and own.any()
 
 
-def test_pageable_gather_runs_per_shard_in_parallel(monkeypatch):
+@pytest.mark.parametrize("staged", ["1", "0"])
+def test_pageable_gather_runs_per_shard_in_parallel(monkeypatch, staged):
     """Pageable arenas over 2 shards: one gather/issue thread per GPU, so the
     host copies for the two shards overlap in time instead of alternating on
-    one thread (msha_shard_stats gather windows)."""
+    one thread (msha_shard_stats gather windows) -- on the staged direct path
+    and on the gather pipeline (MSHA_STAGED_DIRECT=0)."""
     from mirbft_amd import Engine
     monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", "2")
+    monkeypatch.setenv("MSHA_STAGED_DIRECT", staged)
     w = W.c2_requests(1 << 20)                  # 512 MiB: 8 staging chunks per shard
     with Engine(1) as e:
         got = e.digest_batch(w.arena, w.off, w.len)
