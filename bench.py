@@ -53,6 +53,20 @@ OPS_PER_BLOCK = 1400           # DESIGN.md "Algorithmic work per block"
 BARE_LOOP_TOPS = 28.3e9 * OPS_PER_BLOCK / 1e12
 PEAK_VALU_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # 78.64 T int32 lane-ops/s
 METRIC = "SHA-256 digests/sec + GB/s hashed (1/2/4/8 MI355X), % integer-ALU roofline"
+# BASELINE config 5's device-resident forms: c5 = the caller's size-class order
+# (msha_order_by_blocks on the host, once, as part of packing), every action
+# hashed; c5_planned = msha_digest_batch_device_planned, the order planned on
+# the GPU inside every timed step, longest chains on the cooperative kernel
+# beside the lane kernel; c5_folded = the same with alias folding (equal
+# (off, len) hashed once per step, every action still gets its digest).
+C5_FORMS = ("c5", "c5_planned", "c5_folded")
+C5_FORM_NOTES = {
+    "c5": "caller's size-class order (host, once, part of packing); every action hashed",
+    "c5_planned": "msha_digest_batch_device_planned: order planned on the GPU inside each step, longest "
+                  "chains on the cooperative kernel on CUs of their own; every action hashed",
+    "c5_folded": "msha_digest_batch_device_planned + MSHA_PLAN_FOLD_ALIASES: the same, equal (off, len) "
+                 "hashed once per step and the digest copied to every such action (frac on hashed blocks)",
+}
 
 
 def parse():
@@ -101,7 +115,7 @@ def build_workload(cfg: str, rank: int, world: int):
     if cfg == "c4":
         n = 65536
         return W.c4_large(n=n, first=rank * n)
-    if cfg == "c5":
+    if cfg in C5_FORMS:
         total = 1 << 23
         per = total // world            # c5 is quoted as 8M actions over the node
         return W.c5_storm(n=per, first=rank * per)
@@ -289,6 +303,12 @@ def kernel_step(eng, w, cfg: str, dev, stream):
         return step, d_out
     d_off = torch.from_numpy(w.off.view(np.int64)).to(dev)
     d_len = torch.from_numpy(w.len.view(np.int64)).to(dev)
+    if cfg in ("c5_planned", "c5_folded"):
+        fold = cfg == "c5_folded"
+
+        def step():
+            eng.digest_batch_device_planned(d_arena, d_off, d_len, d_out, stream, fold=fold)
+        return step, d_out
     d_order = None
     if not w.uniform_stride:
         # mixed sizes: the packer's size-class order (host, once; part of packing)
@@ -357,8 +377,19 @@ def algorithmic_bytes(w, cfg: str) -> int:
     return w.message_bytes + meta + 32 * w.n
 
 
+def hashed_blocks(w, cfg: str) -> int:
+    """Blocks one launch compresses: every message's, or with alias folding
+    (c5_folded) each distinct (off, len) once."""
+    if cfg != "c5_folded":
+        return w.blocks
+    key = np.stack([w.off, w.len], axis=1)
+    uniq = np.unique(key, axis=0)
+    L = uniq[:, 1]
+    return int(((L >> np.uint64(6)) + np.where((L & np.uint64(63)) < 56, 1, 2).astype(np.uint64)).sum())
+
+
 def roofline(w, kern_ms: float, cfg: str) -> dict:
-    achieved = OPS_PER_BLOCK * w.blocks / (kern_ms * 1e-3) / 1e12
+    achieved = OPS_PER_BLOCK * hashed_blocks(w, cfg) / (kern_ms * 1e-3) / 1e12
     traffic, src = measured_traffic(cfg)
     return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS,
             "unit": "Tint32op/s", "frac": achieved / PEAK_VALU_TOPS,
@@ -372,12 +403,14 @@ def roofline(w, kern_ms: float, cfg: str) -> dict:
             "frac_of_bare_loop": achieved / BARE_LOOP_TOPS}
 
 
-def extra_config(eng, cfg: str, args, dev, stream) -> dict:
+def extra_config(eng, cfg: str, args, dev, stream, w=None) -> dict:
     """One more config timed like the headline (kernel-resident, same warmup and
     K), with its own roofline fraction and a verified sample: puts c3/c4 under
-    the driver's clock next to c2 (c3, c4 and c5 in the default run)."""
+    the driver's clock next to c2 (c3, c4 and c5's three forms in the default
+    run; w: a workload already built, shared by the c5 forms)."""
     import torch
-    w = build_workload(cfg, 0, 1)
+    if w is None:
+        w = build_workload(cfg, 0, 1)
     step, d_out = kernel_step(eng, w, cfg, dev, stream)
     st0 = eng.stats()
     elapsed, kern_ms, warm, warmup_ms = time_steps(step, args, dev, stream)
@@ -389,22 +422,27 @@ def extra_config(eng, cfg: str, args, dev, stream) -> dict:
            "gbps_hashed": w.message_bytes * args.steps / elapsed / 1e9,
            "ms_per_step": elapsed / args.steps * 1e3, "kernel_ms_mean": kern_ms, "kernel": kind,
            "frac": rf["frac"], "achieved": rf["achieved"], "traffic": rf["traffic"],
-           "blocks": w.blocks, "verified": "512 digests vs oracle (stride not a multiple of 64)",
+           "blocks": w.blocks, "hashed_blocks": hashed_blocks(w, cfg),
+           "verified": "512 digests vs oracle (stride not a multiple of 64)",
            "warmup_steps_run": warm}
+    if cfg in C5_FORMS:
+        out["form"] = C5_FORM_NOTES[cfg]
     del step, d_out
     torch.cuda.empty_cache()
     return out
 
 
-def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist) -> dict:
+def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist, form: str = "c5", w=None) -> dict:
     """BASELINE config c5 as quoted -- the node's 2^23-action storm split over the
     job's GPUs (strong scaling: each rank hashes its 2^23 / N slice, the same
     generator stream bench.py's one-GPU c5 leg uses) -- kernel-resident, timed
     like the headline: barrier + synchronize around K launches per rank, the max
-    over ranks. Every rank verifies 512 of its digests against the oracle."""
+    over ranks, in one of the C5_FORMS. Every rank verifies 512 of its digests
+    against the oracle."""
     import torch
-    w = build_workload("c5", rank, world)
-    step, d_out = kernel_step(eng, w, "c5", dev, stream)
+    if w is None:
+        w = build_workload("c5", rank, world)
+    step, d_out = kernel_step(eng, w, form, dev, stream)
     st0 = eng.stats()
     elapsed, kern_ms, warm, _ = time_steps(step, args, dev, stream, barrier=dist.barrier)
     dist.barrier()
@@ -414,18 +452,20 @@ def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist) -> dict:
     t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     elapsed, kern_max = (float(x) for x in t.tolist())
-    tot = torch.tensor([w.n, w.message_bytes, w.blocks], dtype=torch.float64)
+    tot = torch.tensor([w.n, w.message_bytes, w.blocks, hashed_blocks(w, form)], dtype=torch.float64)
     dist.all_reduce(tot)
-    n, nbytes, blocks = (float(x) for x in tot.tolist())
+    n, nbytes, blocks, hashed = (float(x) for x in tot.tolist())
     del step, d_out
     torch.cuda.empty_cache()
-    achieved = OPS_PER_BLOCK * blocks / (kern_max * 1e-3) / 1e12      # all GPUs, slowest rank's launch
+    achieved = OPS_PER_BLOCK * hashed / (kern_max * 1e-3) / 1e12      # all GPUs, slowest rank's launch
     return {"workload": f"c5: {1 << 23} mixed actions (70/25/5) over {world} GPUs, {w.n} per GPU",
+            "form": C5_FORM_NOTES[form],
             "n_gpus": world, "scaling": "strong", "value": n * args.steps / elapsed, "unit": "digests/s",
             "gbps_hashed": nbytes * args.steps / elapsed / 1e9, "ms_per_step": elapsed / args.steps * 1e3,
             "kernel_ms_mean_max_over_ranks": kern_max, "kernel": kind,
             "frac": achieved / (PEAK_VALU_TOPS * world), "achieved": achieved, "peak": PEAK_VALU_TOPS * world,
-            "blocks": int(blocks), "verified": "512 digests per rank vs oracle (stride not a multiple of 64)",
+            "blocks": int(blocks), "hashed_blocks": int(hashed),
+            "verified": "512 digests per rank vs oracle (stride not a multiple of 64)",
             "warmup_steps_run": warm}
 
 
@@ -556,7 +596,7 @@ def main():
             "warmup_ms": warmup_ms,
             "ms_per_step": elapsed / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "strong" if args.config == "c5" else "weak",  # c5: 8M actions per node
+            "scaling": "strong" if args.config in C5_FORMS else "weak",  # c5: 8M actions per node
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (splitmix64 seed 0x4D49524246540000), inputs resident in HBM",
@@ -571,14 +611,20 @@ def main():
         if world == 1 and args.config == "c2" and not args.no_extra:
             del step, d_out
             torch.cuda.empty_cache()
-            line["extra_configs"] = {c: extra_config(eng, c, args, dev, stream) for c in ("c3", "c4", "c5")}
+            line["extra_configs"] = {c: extra_config(eng, c, args, dev, stream) for c in ("c3", "c4")}
+            w5 = build_workload("c5", 0, 1)
+            for c in C5_FORMS:
+                line["extra_configs"][c] = extra_config(eng, c, args, dev, stream, w5)
+            del w5
     if world > 1 and args.config == "c2" and not args.no_extra:
         # every rank takes part: c5 is quoted over the node's GPUs (BASELINE config 5)
         del step, d_out
         torch.cuda.empty_cache()
-        c5 = extra_c5_ranks(eng, args, dev, stream, rank, world, dist)
+        w5 = build_workload("c5", rank, world)
+        c5 = {c: extra_c5_ranks(eng, args, dev, stream, rank, world, dist, c, w5) for c in C5_FORMS}
+        del w5
         if rank == 0:
-            line["extra_configs"] = {"c5": c5}
+            line["extra_configs"] = c5
     eng.close()
     if world > 1:
         dist.barrier()              # every rank has released its GPU

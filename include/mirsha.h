@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 6u
+#define MSHA_ABI_VERSION 7u
 
 enum {
   MSHA_OK = 0,
@@ -91,6 +91,7 @@ typedef struct {
   uint64_t staged_calls;    /* host calls whose pageable arena had the direct path's shape (16-B aligned,
                                dense): its touched runs went up through pinned staging, lanes planned
                                on the GPU (ABI 6) */
+  uint64_t planned_device_calls; /* msha_digest_batch_device_planned calls (ABI 7) */
 } msha_stats;
 
 /* Per-GPU figures of the last host-memory call (one entry per shard; a shard is
@@ -196,6 +197,22 @@ int msha_digest_of_digests(msha_ctx* ctx, const uint8_t* table, uint64_t n_table
 int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
                              const uint64_t* d_len, const uint32_t* d_order, uint64_t n,
                              uint8_t* d_out, void* stream);
+/*
+ * The same messages, planned on the GPU inside the call's own launches (no host
+ * round trip, nothing precomputed by the caller): lanes are ordered by
+ * descending block count; with MSHA_PLAN_FOLD_ALIASES, messages with equal
+ * (d_off, d_len) -- EpochChange payloads re-hashed N^2 times,
+ * epoch_target.go:486-505 -- are hashed once and the digest copied to every
+ * such slot; and the longest chains, when one alone would outlast the rest of
+ * the launch (a mixed storm sharded over several GPUs), run on the cooperative
+ * kernel beside the lane kernel (a side stream forked from and joined back to
+ * `stream`). Same arena rules and error reporting as msha_digest_batch_device;
+ * n < 2^32 - 1. Returns after enqueueing.
+ */
+enum { MSHA_PLAN_FOLD_ALIASES = 1u };
+int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                                     const uint64_t* d_len, uint64_t n, uint32_t flags, uint8_t* d_out,
+                                     void* stream);
 /* Uniform layout: message i = d_arena[i*stride : i*stride + msg_len] (stride a
  * multiple of 16; messages may overlap, stride 0 hashes one message n times). */
 int msha_digest_uniform_device(msha_ctx* ctx, const uint8_t* d_arena, uint64_t stride,

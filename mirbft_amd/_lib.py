@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -54,6 +54,7 @@ class MshaStats(ctypes.Structure):
         ("d2h_bytes", ctypes.c_uint64),
         ("small_calls", ctypes.c_uint64),
         ("staged_calls", ctypes.c_uint64),
+        ("planned_device_calls", ctypes.c_uint64),
     ]
 
 
@@ -100,6 +101,9 @@ SIGNATURES = {
     "msha_digest_batch_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                 ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                                 ctypes.c_void_p]),
+    "msha_digest_batch_device_planned": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_void_p,
+                                                        ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                                        ctypes.c_void_p, ctypes.c_void_p]),
     "msha_digest_uniform_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64,
                                                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]),
     "msha_digest_of_digests_device": (ctypes.c_int, [_ctxp, ctypes.c_void_p, ctypes.c_void_p,

@@ -253,10 +253,17 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
                                                       const uint32_t* __restrict__ order,
                                                       const uint32_t* __restrict__ out_idx,
                                                       uint64_t n, uint8_t* __restrict__ out,
-                                                      uint32_t* __restrict__ err) {
+                                                      uint32_t* __restrict__ err,
+                                                      const uint32_t* __restrict__ skip_below) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t m = order ? (uint64_t)order[i] : i;      // metadata index
+  if (skip_below && i < *skip_below) return;  // a long chain: the cooperative launch has it
+  uint64_t m = i;                             // metadata index
+  if (order) {
+    const uint32_t v = order[i];
+    if (v == kNoLane) return;                 // planned launch: a folded alias's position
+    m = v;
+  }
   const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;  // digest slot
   const uint8_t* p = arena + off[m];
   if (check_aligned(p, out + 32 * o, err))
@@ -271,10 +278,17 @@ __global__ __launch_bounds__(256) void k_digest_batch_pipe(const uint8_t* __rest
                                                            const uint32_t* __restrict__ order,
                                                            const uint32_t* __restrict__ out_idx,
                                                            uint64_t n, uint8_t* __restrict__ out,
-                                                           uint32_t* __restrict__ err) {
+                                                           uint32_t* __restrict__ err,
+                                                           const uint32_t* __restrict__ skip_below) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
-  const uint64_t m = order ? (uint64_t)order[i] : i;
+  if (skip_below && i < *skip_below) return;
+  uint64_t m = i;
+  if (order) {
+    const uint32_t v = order[i];
+    if (v == kNoLane) return;
+    m = v;
+  }
   const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;
   const uint8_t* p = arena + off[m];
   if (check_aligned(p, out + 32 * o, err))
@@ -757,17 +771,23 @@ __device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], uint4* __restrict
 // gets a SIMD of its own; the launch reserves enough LDS (kCoopLdsBytes) that
 // a CU holds ONE such workgroup, so a consumer never shares its SIMD with
 // another consumer (that would forfeit the latency gain).
-constexpr unsigned kCoopMsgsPerWg = 128;
 constexpr size_t kCoopDynLds = 40 * 1024;  // + 64 KiB static = 104 KiB > 160/2 KiB
 
-template <int MODE>
+// EXCL (a planned launch's head): the waves claim every register of their SIMD
+// (an empty asm clobbering v255 and a255: 512 per lane), so a CU running a
+// head workgroup holds nothing else -- lane-kernel waves beside it would
+// either stall the chain (their older waves win issue) or, with the head at
+// top priority, be starved themselves for the whole chain (c5 over 4 GPUs:
+// 5.0 -> 6.4 ms). The head's CUs run the head; the lane kernel has the rest.
+template <int MODE, bool EXCL = false>
 __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__ arena,
                                                      const uint64_t* __restrict__ off,
                                                      const uint64_t* __restrict__ len,
                                                      const uint32_t* __restrict__ order,
                                                      const uint32_t* __restrict__ out_idx,
                                                      uint64_t n, uint8_t* __restrict__ out,
-                                                     uint32_t* __restrict__ err) {
+                                                     uint32_t* __restrict__ err,
+                                                     const uint32_t* __restrict__ limit) {
   __shared__ uint4 kw[2][2][kCoopSlotQuads * 64];  // [slot][group][quad][lane]: 64 KiB
   __shared__ uint32_t s_nb;
   const unsigned lane = threadIdx.x & 63;
@@ -775,8 +795,20 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
   const bool producer = wave >= 2;
   const unsigned group = wave & 1;
   const uint64_t i = (uint64_t)blockIdx.x * kCoopMsgsPerWg + group * 64 + lane;
-  bool active = i < n;
-  const uint64_t m = active ? (order ? (uint64_t)order[i] : i) : 0;  // metadata index
+  // limit: a planned launch's head of long chains ends at *limit (device-side).
+  // That launch runs beside the lane kernel, whose older waves would win issue
+  // arbitration on the SIMDs it shares with them (a chain then crawls at a
+  // fraction of its rate): the head's waves take the highest issue priority.
+  if (EXCL) asm volatile("" ::: "v255", "a255");
+  if (limit) __builtin_amdgcn_s_setprio(3);
+  bool active = i < n && (!limit || i < *limit);
+  uint64_t m = i;  // metadata index
+  if (active && order) {
+    const uint32_t v = order[i];
+    active = v != kNoLane;
+    m = active ? v : 0;
+  }
+  if (!active) m = 0;
   const uint64_t o = active ? (out_idx ? (uint64_t)out_idx[i] : m) : 0;  // digest slot
   const uint8_t* p = arena;
   uint64_t L = 0;
@@ -961,10 +993,18 @@ static inline void set_kind(LaunchKind* kind, LaunchKind k) {
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
                                const uint32_t* order, const uint32_t* out_idx, uint64_t n,
                                uint8_t* out, uint32_t* err, int cus, int policy, hipStream_t st,
-                               const SplitPlan* split, LaunchKind* kind) {
+                               const SplitPlan* split, LaunchKind* kind, const LaneGate* gate) {
   set_kind(kind, kLaunchNone);
   if (n == 0) return hipSuccess;
-  if (split) {
+  const uint32_t* head = gate ? gate->head : nullptr;
+  if (gate && gate->head_part) {  // the planned launch's long chains: cooperative, up to *head
+    const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
+    hipLaunchKernelGGL((k_digest_coop<kPrefetch, true>), dim3(grid), dim3(256), kCoopDynLds, st, arena, off,
+                       len, order, out_idx, n, out, err, head);
+    set_kind(kind, kLaunchCoop);
+    return hipGetLastError();
+  }
+  if (split && !gate) {
     const unsigned grid = split->segments * split->groups + (unsigned)(split->n_main / 256);
     const ArenaSrc src{arena, off, len, order, out_idx, err};
     with_mode(split_mode(*split, cus), [&](auto m) {
@@ -974,23 +1014,23 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
     set_kind(kind, kLaunchSplit);
     return hipGetLastError();
   }
-  if (uses_coop(n, cus, policy)) {
+  if (uses_coop(n, cus, policy) && !head) {
     const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
     hipLaunchKernelGGL(k_digest_coop<kPrefetch>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len,
-                       order, out_idx, n, out, err);
+                       order, out_idx, n, out, err, nullptr);
     set_kind(kind, kLaunchCoop);
     return hipGetLastError();
   }
   const int mode = pick_mode(n, cus);
   if (mode == kPipe) {
     hipLaunchKernelGGL(k_digest_batch_pipe, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
-                       order, out_idx, n, out, err);
+                       order, out_idx, n, out, err, head);
     set_kind(kind, kLaunchPipe);
     return hipGetLastError();
   }
   with_mode(mode, [&](auto m) {
     hipLaunchKernelGGL(k_digest_batch<decltype(m)::value>, dim3(grid_for(n)), dim3(256), 0, st,
-                       arena, off, len, order, out_idx, n, out, err);
+                       arena, off, len, order, out_idx, n, out, err, head);
   });
   set_kind(kind, kLaunchLane);
   return hipGetLastError();

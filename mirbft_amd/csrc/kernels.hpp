@@ -35,12 +35,27 @@ bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp, int cap);
 // Which kernel a launcher ran (msha_stats launch counters; tests assert them).
 enum LaunchKind { kLaunchNone = 0, kLaunchLane, kLaunchPipe, kLaunchCoop, kLaunchSplit, kLaunchDod };
 
+// GPU-planned device launches (plan.hip: msha_digest_batch_device_planned). The
+// planner's lane order holds kNoLane at positions it leaves unused (folded
+// aliases, at the end), and *head (device memory, known only on the GPU) lanes
+// at the front are long chains routed to the cooperative kernel. A gated launch
+// over the whole order either is that head (head_part: cooperative, lanes at or
+// past *head idle) or the rest (lanes below *head idle); neither splits.
+constexpr uint32_t kNoLane = 0xFFFFFFFFu;
+struct LaneGate {
+  const uint32_t* head = nullptr;
+  bool head_part = false;
+};
+
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
                                const uint32_t* order, const uint32_t* out_idx, uint64_t n,
                                uint8_t* out, uint32_t* err, int cus, int policy, hipStream_t st,
-                               const SplitPlan* split = nullptr, LaunchKind* kind = nullptr);
+                               const SplitPlan* split = nullptr, LaunchKind* kind = nullptr,
+                               const LaneGate* gate = nullptr);
 // Does launch_digest_batch use cooperative chaining for an n-message launch?
 bool uses_coop(uint64_t n, int cus, int policy);
+// Messages per workgroup of the cooperative kernel (one workgroup per CU).
+constexpr unsigned kCoopMsgsPerWg = 128;
 hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st, LaunchKind* kind = nullptr);
@@ -82,5 +97,41 @@ struct PlanArgs {
   uint32_t* lane_slot;
 };
 hipError_t launch_plan(const PlanArgs& a, hipStream_t st);
+
+// Device-side planning of a device-resident batch (plan.hip,
+// msha_digest_batch_device_planned): every array is device memory of one GPU.
+// Lanes = messages, or with a table only the first of each (off, len) key
+// (aliases fold into it); the order lists lanes by descending block count,
+// kNoLane past the last; info[1] = the head of lanes whose chains would outlast
+// the lane kernel's throughput time, for the cooperative kernel (at most
+// head_cap). Block-count buckets: exact below 4,096 blocks, powers of two above.
+constexpr uint32_t kFoldBuckets = 4096 + 52;
+struct FoldArgs {
+  const uint64_t* off;
+  const uint64_t* len;
+  uint64_t n = 0;
+  uint32_t* table = nullptr;  // tmask + 1 zeroed entries; null: no folding
+  uint64_t tmask = 0;
+  uint32_t* rep = nullptr;    // n (with table): the lane message i's digest comes from
+  uint64_t* tmax = nullptr;   // (with table) ceil(n / 4096): largest offset before each tile
+  uint32_t* cnt;              // kFoldBuckets zeroed counters -> bucket starts
+  uint32_t* order;            // n, kNoLane-filled -> position -> message index
+  uint32_t* info;             // out: [0] lanes, [1] head
+  uint32_t head_cap = 0;      // 0: no head
+  uint32_t simds = 1024;
+  // The head: the cut of the longest lanes that minimises the launch's
+  // estimated end (plan.hip head_cost). SIMD cycles per block, measured (c5
+  // slices, rocprofv3 timelines, profiles/r03_planned/): a lane-kernel wave
+  // among 8 per SIMD ~5,700 per wave-block; a long chain on the lane kernel
+  // ~7,000 (the oldest wave of its SIMD); on the cooperative kernel, alone on
+  // its CU at top priority, ~4,200. head_pct scales the head's term (A/B).
+  uint32_t wave_block_cycles = 5700;
+  uint32_t lane_cycles = 7000;
+  uint32_t coop_cycles = 4200;
+  uint32_t head_pct = 100;
+};
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st);
+// out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.
+hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st);
 
 }  // namespace msha

@@ -234,6 +234,12 @@ struct Device {
   // [gmin | cut | info] read back to h_small; rep read back to h_rep
   DevBuf p_meta, p_gmap, p_devoff, p_table, p_slot, p_rep, p_cnt, p_small;
   PinBuf h_gmap, h_small, h_rep;
+  // planned device calls (msha_digest_batch_device_planned): alias table,
+  // representatives, bucket counters, lane order, [lanes | head]; the head of
+  // long chains runs on side_stream, forked from and joined to the caller's
+  DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_info;
+  hipStream_t side_stream = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_fplan = nullptr, ev_join = nullptr;
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
@@ -251,14 +257,15 @@ struct Device {
   void release() {
     gather_pool.reset();
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table, &sm_in, &sm_out, &p_meta,
-                      &p_gmap, &p_devoff, &p_table, &p_slot, &p_rep, &p_cnt, &p_small})
+                      &p_gmap, &p_devoff, &p_table, &p_slot, &p_rep, &p_cnt, &p_small, &f_table, &f_rep,
+                      &f_tmax, &f_cnt, &f_order, &f_info})
       b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
     for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1], &sm_stage, &sm_res, &h_gmap, &h_small, &h_rep})
       b->release();
     for (hipEvent_t* e : {&ev0, &ev1, &ev_up0, &ev_up1, &ev_k0, &ev_meta, &ev_plan, &ev_p0, &ev_p1, &slot_free[0],
-                          &slot_free[1], &chunk_in}) {
+                          &slot_free[1], &chunk_in, &ev_fork, &ev_fplan, &ev_join}) {
       if (*e) (void)hipEventDestroy(*e);
       *e = nullptr;
     }
@@ -267,9 +274,10 @@ struct Device {
     if (stream) (void)hipStreamDestroy(stream);
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
+    if (side_stream) (void)hipStreamDestroy(side_stream);
     if (ev_k) (void)hipEventDestroy(ev_k);
     ev_k = nullptr;
-    stream = copy_stream = d2h_stream = nullptr;
+    stream = copy_stream = d2h_stream = side_stream = nullptr;
   }
 };
 
@@ -2480,6 +2488,108 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
                                      d.err.as<uint32_t>(), d.cus, ctx->kernel_policy, st,
                                      split_for(d, n, ctx->kernel_policy, sp), &kind));
     count_launch(ctx, nullptr, kind);
+  });
+}
+
+int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
+                                     const uint64_t* d_len, uint64_t n, uint32_t flags, uint8_t* d_out,
+                                     void* stream) {
+  if (!ctx) return MSHA_ERR_INVALID_ARG;
+  if (n == 0) return MSHA_OK;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
+  if (!d_arena || !d_off || !d_len || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
+  if (flags & ~(uint32_t)MSHA_PLAN_FOLD_ALIASES) return fail(ctx, MSHA_ERR_INVALID_ARG, "unknown plan flags");
+  if (n >= msha::kNoLane) return fail(ctx, MSHA_ERR_INVALID_ARG, "planned device batches hold < 2^32 - 1 messages");
+  return guarded(ctx, [&] {
+    hipStream_t st;
+    device_prologue(ctx, stream, &st);
+    Device& d = ctx->devs[0];
+    const bool fold = flags & MSHA_PLAN_FOLD_ALIASES;
+    // Few messages: one cooperative launch over the planned order (every
+    // workgroup gets a CU); otherwise the lane kernel, its longest chains
+    // (if any outlast the launch) on the cooperative kernel beside it.
+    const bool all_coop = msha::uses_coop(n, d.cus, ctx->kernel_policy);
+    const bool head = !all_coop && ctx->kernel_policy != MSHA_KERNEL_LANE && env_u64("MSHA_PLAN_HEAD", 1) != 0;
+    uint64_t cap = 1024;
+    while (cap < 2 * n) cap <<= 1;
+    d.f_cnt.ensure(4 * msha::kFoldBuckets);
+    d.f_order.ensure(4 * n);
+    d.f_info.ensure(8);
+    if (fold) {
+      d.f_table.ensure(4 * cap);
+      d.f_rep.ensure(4 * n);
+      d.f_tmax.ensure(8 * ((n + 4095) / 4096));
+    }
+    // With a head, the planner and then the head's cooperative launch run on
+    // the side stream, and the lane kernel on `stream` waits for the planner's
+    // event: the head's packet follows the planner in its own queue while the
+    // lane kernel's needs a cross-queue signal, so the head's workgroups are
+    // resident before the lane kernel fills every SIMD (queued the other way
+    // round, the head could not get a CU's registers until the lane kernel
+    // drained: c5 folded 6.2 ms, its 1,427-block chain starting at the end).
+    hipStream_t ps = st;
+    if (head) {
+      if (!d.side_stream) HIPCHK(hipStreamCreateWithFlags(&d.side_stream, hipStreamNonBlocking));
+      for (hipEvent_t* e : {&d.ev_fork, &d.ev_fplan, &d.ev_join})
+        if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      HIPCHK(hipEventRecord(d.ev_fork, st));
+      HIPCHK(hipStreamWaitEvent(d.side_stream, d.ev_fork, 0));
+      ps = d.side_stream;
+    }
+    if (fold) HIPCHK(hipMemsetAsync(d.f_table.p, 0, 4 * cap, ps));
+    HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, 4 * msha::kFoldBuckets, ps));
+    HIPCHK(hipMemsetAsync(d.f_order.p, 0xFF, 4 * n, ps));  // kNoLane
+    msha::FoldArgs fa;
+    fa.off = d_off;
+    fa.len = d_len;
+    fa.n = n;
+    fa.table = fold ? d.f_table.as<uint32_t>() : nullptr;
+    fa.tmask = cap - 1;
+    fa.rep = fold ? d.f_rep.as<uint32_t>() : nullptr;
+    fa.tmax = fold ? d.f_tmax.as<uint64_t>() : nullptr;
+    fa.cnt = d.f_cnt.as<uint32_t>();
+    fa.order = d.f_order.as<uint32_t>();
+    fa.info = d.f_info.as<uint32_t>();
+    fa.simds = (uint32_t)d.cus * 4;
+    fa.head_cap = head ? (uint32_t)std::min<uint64_t>(n, (uint64_t)d.cus * msha::kCoopMsgsPerWg) : 0;
+    fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
+    HIPCHK(msha::launch_fold_plan(fa, ps));
+    const uint32_t* order = d.f_order.as<uint32_t>();
+    msha::LaunchKind kind;
+    if (all_coop) {
+      HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, order, nullptr, n, d_out, d.err.as<uint32_t>(),
+                                       d.cus, MSHA_KERNEL_COOP, st, nullptr, &kind));
+      count_launch(ctx, nullptr, kind);
+    } else {
+      msha::LaneGate body;
+      body.head = fa.info + 1;
+      if (head) {
+        HIPCHK(hipEventRecord(d.ev_fplan, d.side_stream));
+        msha::LaneGate hg;
+        hg.head = fa.info + 1;
+        hg.head_part = true;
+        HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, order, nullptr, fa.head_cap, d_out,
+                                         d.err.as<uint32_t>(), d.cus, MSHA_KERNEL_COOP, d.side_stream, nullptr,
+                                         &kind, &hg));
+        count_launch(ctx, nullptr, kind);
+        HIPCHK(hipEventRecord(d.ev_join, d.side_stream));
+        HIPCHK(hipStreamWaitEvent(st, d.ev_fplan, 0));
+      }
+      HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, order, nullptr, n, d_out, d.err.as<uint32_t>(),
+                                       d.cus, ctx->kernel_policy, st, nullptr, &kind, &body));
+      count_launch(ctx, nullptr, kind);
+      if (head) HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
+    }
+    if (fold) HIPCHK(msha::launch_fold_fill(fa.rep, n, d_out, st));
+    ctx->stats.planned_device_calls++;
+    if (trace_on()) {  // MSHA_TRACE: the GPU's plan (waits for the call)
+      uint32_t info[2] = {0, 0};
+      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipMemcpy(info, fa.info, sizeof info, hipMemcpyDeviceToHost));
+      fprintf(stderr, "[msha] planned device call: %llu messages, %u lanes, head %u\n", (unsigned long long)n,
+              info[0], info[1]);
+    }
   });
 }
 

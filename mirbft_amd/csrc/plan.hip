@@ -63,11 +63,15 @@ __global__ __launch_bounds__(256) void k_plan_remap(PlanArgs a) {
   uint64_t h = plan_hash(o, l) & a.tmask;
   const uint32_t me = (uint32_t)i + 1;  // 0 = empty slot
   for (;;) {
-    const uint32_t v = atomicCAS(&a.table[h], 0u, me);
+    // a plain read first: a claimed slot never empties, so a hot key (one
+    // EpochChange payload named by thousands of messages) costs a cached read
+    // per message, not a serialised atomic
+    uint32_t v = __hip_atomic_load(&a.table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0) v = atomicCAS(&a.table[h], 0u, me);
     if (v == 0) break;
     const uint64_t j = v - 1;
     if (a.off[j] == o && a.len[j] == l) {  // same key: the slot keeps the smallest index
-      atomicMin(&a.table[h], me);
+      if (me < v) atomicMin(&a.table[h], me);
       break;
     }
     h = (h + 1) & a.tmask;
@@ -114,6 +118,42 @@ __device__ __forceinline__ uint32_t tile_slot(TileTable& t, uint32_t k) {
   return kPlanSlots;
 }
 
+// Wave-aggregated tile count: the lanes of a wave holding valid keys take one
+// LDS atomic per distinct key among them (a request batch's wave: one), not
+// one per lane -- 64 lanes adding to one LDS word serialise. Calls
+// done(lane's slot, lane's rank) on every valid lane: slot < kPlanSlots is the
+// tile table's entry (rank inside the tile), kPlanSlots the global counter
+// (rank = global position); lanes are ranked in lane order, and the wave's
+// lowest lane of each key is its leader (min_idx: atomicMin of its index into
+// aux, the host planner's lowest lane per piece).
+template <bool kMinAux, class Done>
+__device__ __forceinline__ void wave_count(TileTable& t, uint32_t* gcnt, uint32_t* gmin, uint32_t B,
+                                           bool valid, uint32_t k, uint32_t idx, Done&& done) {
+  uint64_t pend = __ballot(valid);
+  const unsigned lane = __lane_id();
+  while (pend) {
+    const int leader = __ffsll((long long)pend) - 1;
+    const uint32_t k0 = __shfl(k, leader);
+    const uint64_t same = __ballot(valid && k == k0) & pend;
+    uint32_t j = 0, base = 0;
+    if ((int)lane == leader) {
+      const uint32_t c = (uint32_t)__popcll(same);
+      j = tile_slot(t, k0);
+      if (j < kPlanSlots) {
+        base = atomicAdd(&t.cnt[j], c);
+        if (kMinAux) atomicMin(&t.aux[j], idx);
+      } else {
+        base = atomicAdd(&gcnt[k0], c);
+        if (kMinAux) atomicMin(&gmin[k0 / B], idx);
+      }
+    }
+    j = __shfl(j, leader);
+    base = __shfl(base, leader);
+    if ((same >> lane) & 1) done(j, base + (uint32_t)__popcll(same & ((1ull << lane) - 1)));
+    pend &= ~same;
+  }
+}
+
 // Bucket key of message i when it is a lane (rep[i] == i): (piece holding the
 // payload's end) * B + (bmax - blocks).
 __device__ __forceinline__ uint32_t lane_key(const PlanArgs& a, uint64_t i, uint32_t* chunk_out) {
@@ -132,20 +172,16 @@ __global__ __launch_bounds__(256) void k_plan_keys(PlanArgs a) {
 #pragma unroll 4
   for (uint32_t r = 0; r < kPlanItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    if (i >= a.m) break;
-    const uint32_t rp = a.table ? a.table[a.slot[i]] - 1 : (uint32_t)i;
-    a.rep[i] = rp;
-    if (rp != (uint32_t)i) continue;
-    uint32_t chunk;
-    const uint32_t k = lane_key(a, i, &chunk);
-    const uint32_t j = tile_slot(t, k);
-    if (j < kPlanSlots) {
-      atomicAdd(&t.cnt[j], 1u);
-      atomicMin(&t.aux[j], (uint32_t)i);
-    } else {  // table full: straight to the global counters
-      atomicAdd(&a.cnt[k], 1u);
-      atomicMin(&a.gmin[chunk], (uint32_t)i);
+    bool lane_ok = i < a.m;
+    uint32_t k = 0;
+    if (lane_ok) {
+      const uint32_t rp = a.table ? a.table[a.slot[i]] - 1 : (uint32_t)i;
+      a.rep[i] = rp;
+      lane_ok = rp == (uint32_t)i;
+      if (lane_ok) k = lane_key(a, i, nullptr);
     }
+    // table full: straight to the global counters (lowest lane per piece)
+    wave_count<true>(t, a.cnt, a.gmin, (uint32_t)a.B, lane_ok, k, (uint32_t)i, [](uint32_t, uint32_t) {});
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < kPlanSlots; j += blockDim.x) {
@@ -199,16 +235,13 @@ __global__ __launch_bounds__(256) void k_plan_scatter(PlanArgs a) {
   for (uint32_t r = 0; r < kPlanItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
     slot[r] = kEmptyKey;
-    if (i >= a.m || a.rep[i] != (uint32_t)i) continue;
-    const uint32_t k = lane_key(a, i, nullptr);
-    const uint32_t j = tile_slot(t, k);
-    if (j < kPlanSlots) {
+    const bool lane_ok = i < a.m && a.rep[i] == (uint32_t)i;
+    const uint32_t k = lane_ok ? lane_key(a, i, nullptr) : 0u;
+    // table full (slot kPlanSlots): a position straight from the global counter
+    wave_count<false>(t, a.cnt, nullptr, 1, lane_ok, k, 0, [&](uint32_t j, uint32_t rk) {
       slot[r] = j;
-      rank[r] = atomicAdd(&t.cnt[j], 1u);
-    } else {  // table full: a position straight from the global counter
-      slot[r] = kPlanSlots;
-      rank[r] = atomicAdd(&a.cnt[k], 1u);
-    }
+      rank[r] = rk;
+    });
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < kPlanSlots; j += blockDim.x)
@@ -233,6 +266,316 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t st) {
   hipLaunchKernelGGL(k_plan_keys, dim3(tiles), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_plan_scan, dim3(1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(k_plan_scatter, dim3(tiles), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Device-resident batches (msha_digest_batch_device_planned): the same tile-
+// aggregated bucket sort, over the caller's device arrays, with no host round
+// trip. The lane count and the head of long chains stay on the GPU (info[]):
+// the hash launches read them (kernels.hpp LaneGate), so the whole call is
+// enqueued at once.
+//
+//   k_fold_tilemax, k_fold_tilescan, k_fold_insert   (folding only) messages
+//                   that may repeat an earlier payload claim (off, len) in an
+//                   open-addressing table; the claimer is the key's lane (any one
+//                   will do: the digest is the same), rep[i] = that lane
+//   k_fold_keys     lanes counted per descending block-count bucket
+//   k_fold_scan     one workgroup: bucket starts, lanes, the batch's lane blocks,
+//                   its longest chain, and the head: lanes whose chain on the
+//                   lane kernel would outlast the launch's floor (FoldArgs)
+//   k_fold_scatter  order[position] = message
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t fold_bucket(uint64_t blocks) {  // ascending class
+  if (blocks < 4096) return (uint32_t)blocks;
+  return 4096u + (uint32_t)(63 - __clzll((long long)blocks)) - 12u;
+}
+__device__ __forceinline__ uint64_t fold_bucket_blocks(uint32_t b) {  // lower bound
+  return b < 4096 ? b : (1ull << (b - 4096 + 12));
+}
+__device__ __forceinline__ uint32_t fold_key(uint64_t len) {  // descending block count
+  return kFoldBuckets - 1 - fold_bucket(dev_blocks_for(len));
+}
+
+// Candidates first (the host path's rule, msha_alias_first): a message whose
+// offset is above every earlier message's cannot repeat an earlier payload, so
+// it is its own lane without touching the table; only the others (a storm's
+// EpochChange re-hashes: 5 %) probe and claim. A key first named by a
+// non-candidate and then by candidates is hashed twice -- once for the
+// non-candidate, once for the candidates' claimant -- with the same digest.
+// Tiles of kFoldTile messages, 16 consecutive per thread; tmax[t] = the
+// largest offset of tiles before t (k_fold_tilemax, then k_fold_tilescan).
+__global__ __launch_bounds__(256) void k_fold_tilemax(FoldArgs a) {
+  __shared__ uint64_t part[256];
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile;
+  uint64_t m = 0;
+  for (uint32_t r = 0; r < kPlanItems; ++r) {
+    const uint64_t i = base + r * 256 + threadIdx.x;
+    if (i < a.n) m = max(m, a.off[i]);
+  }
+  part[threadIdx.x] = m;
+  __syncthreads();
+  for (uint32_t d = 128; d > 0; d >>= 1) {
+    if (threadIdx.x < d) part[threadIdx.x] = max(part[threadIdx.x], part[threadIdx.x + d]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.tmax[blockIdx.x] = part[0];
+}
+
+__global__ __launch_bounds__(1024) void k_fold_tilescan(FoldArgs a, uint64_t tiles) {
+  __shared__ uint64_t part[1024];
+  const uint32_t t = threadIdx.x;
+  const uint64_t per = (tiles + 1023) / 1024;
+  const uint64_t b0 = min((uint64_t)t * per, tiles), b1 = min(b0 + per, tiles);
+  uint64_t m = 0;
+  for (uint64_t b = b0; b < b1; ++b) m = max(m, a.tmax[b]);
+  part[t] = m;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive prefix max
+    const uint64_t v = t >= d ? part[t - d] : 0ull;
+    __syncthreads();
+    part[t] = max(part[t], v);
+    __syncthreads();
+  }
+  uint64_t run = t ? part[t - 1] : 0ull;  // exclusive
+  for (uint64_t b = b0; b < b1; ++b) {
+    const uint64_t v = a.tmax[b];
+    a.tmax[b] = run;
+    run = max(run, v);
+  }
+}
+
+__device__ __forceinline__ uint32_t fold_claim(const FoldArgs& a, uint64_t i, uint64_t o, uint64_t l) {
+  uint64_t h = plan_hash(o, l) & a.tmask;
+  const uint32_t me = (uint32_t)i + 1;  // 0 = empty slot
+  for (;;) {
+    // a plain read first: a claimed slot never empties, and a hot key (one
+    // payload named by thousands of messages) then costs a cached read
+    uint32_t v = __hip_atomic_load(&a.table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (v == 0) v = atomicCAS(&a.table[h], 0u, me);
+    if (v == 0) return (uint32_t)i;
+    const uint64_t j = v - 1;
+    if (a.off[j] == o && a.len[j] == l) return (uint32_t)j;
+    h = (h + 1) & a.tmask;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
+  __shared__ uint64_t part[256];
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanItems;
+  uint64_t o[kPlanItems];
+  uint64_t m = 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kPlanItems; ++r) {
+    o[r] = base + r < a.n ? a.off[base + r] : 0;
+    m = max(m, o[r]);
+  }
+  part[threadIdx.x] = m;
+  __syncthreads();
+  for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive prefix max over the tile's threads
+    const uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0ull;
+    __syncthreads();
+    part[threadIdx.x] = max(part[threadIdx.x], v);
+    __syncthreads();
+  }
+  const bool first_ever = blockIdx.x == 0 && threadIdx.x == 0;
+  uint64_t run = max(a.tmax[blockIdx.x], threadIdx.x ? part[threadIdx.x - 1] : 0ull);
+#pragma unroll
+  for (uint32_t r = 0; r < kPlanItems; ++r) {
+    const uint64_t i = base + r;
+    if (i >= a.n) break;
+    const bool fresh = o[r] > run || (first_ever && r == 0);  // above every earlier offset
+    a.rep[i] = fresh ? (uint32_t)i : fold_claim(a, i, o[r], a.len[i]);
+    run = max(run, o[r]);
+  }
+}
+
+// The fold planner's keys are few (kFoldBuckets), so a tile counts them in a
+// directly indexed LDS histogram: one LDS atomic per message, no probing and
+// no per-key wave loop (a storm's wave holds ~15 distinct block counts: the
+// hash-table tile with a wave-aggregated loop per key cost c5's 8.4 M messages
+// 210-270 us per pass, latency-bound).
+constexpr uint32_t kFoldItems = kPlanItems;          // messages per thread
+constexpr uint32_t kFoldTile = 256 * kFoldItems;     // messages per workgroup
+static_assert(kFoldTile <= 4096 && (kFoldBuckets << 12) < kEmptyKey, "scatter packs key << 12 | rank");
+
+__global__ __launch_bounds__(256) void k_fold_keys(FoldArgs a) {
+  __shared__ uint32_t hist[kFoldBuckets];
+  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x) hist[j] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
+#pragma unroll 4
+  for (uint32_t r = 0; r < kFoldItems; ++r) {
+    const uint64_t i = base + r * 256 + threadIdx.x;
+    if (i < a.n && (!a.table || a.rep[i] == (uint32_t)i)) atomicAdd(&hist[fold_key(a.len[i])], 1u);
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
+    if (hist[j]) atomicAdd(&a.cnt[j], hist[j]);
+}
+
+// The head. Per candidate cut k (lanes with keys below k -- the longest -- go
+// to the cooperative kernel, h(k) of them on ceil(h / 128) CUs of their own),
+// the launch's estimated end in SIMD cycles:
+//   T(k) = max( h > 0 ? longest chain x coop_cycles : 0,
+//               remaining lane blocks / 64 / remaining SIMDs x wave_block_cycles,
+//               longest remaining chain x lane_cycles )
+// The cut with the smallest T wins (ties: the smaller head). head_pct scales
+// the head's term (A/B: 1 = a nearly free head, large = none).
+__device__ __forceinline__ uint64_t head_cost(const FoldArgs& a, uint64_t h, uint64_t bh, uint64_t btot,
+                                              uint64_t max_blocks, uint64_t next_blocks) {
+  const uint64_t cus = a.simds / 4, hcus = (h + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg;
+  if (h > a.head_cap || hcus >= cus) return ~0ull;
+  const uint64_t t_head = h ? max_blocks * a.coop_cycles / 100 * a.head_pct : 0;
+  const uint64_t t_body = (btot - bh) * a.wave_block_cycles / (64ull * 4 * (cus - hcus));
+  return max(max(t_head, t_body), next_blocks * a.lane_cycles);
+}
+
+constexpr uint64_t kCostMax = (uint64_t(1) << 40) - 1;
+
+__global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
+  __shared__ uint32_t part[1024];
+  __shared__ uint64_t blk[1024];
+  __shared__ uint64_t best[1024];
+  const uint32_t t = threadIdx.x;
+  constexpr uint32_t per = (kFoldBuckets + 1023) / 1024;
+  const uint32_t b0 = min(t * per, kFoldBuckets), b1 = min(b0 + per, kFoldBuckets);
+  uint32_t s = 0;
+  uint64_t bl = 0;
+  for (uint32_t b = b0; b < b1; ++b) {
+    const uint32_t c = a.cnt[b];
+    s += c;
+    bl += (uint64_t)c * fold_bucket_blocks(kFoldBuckets - 1 - b);
+  }
+  part[t] = s;
+  blk[t] = bl;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive scans of counts and blocks
+    const uint32_t v = t >= d ? part[t - d] : 0u;
+    const uint64_t w = t >= d ? blk[t - d] : 0ull;
+    __syncthreads();
+    part[t] += v;
+    blk[t] += w;
+    __syncthreads();
+  }
+  const uint32_t lanes = part[1023];
+  const uint64_t btot = blk[1023];
+  // longest chain: the first non-empty key (lowest key, most blocks)
+  best[t] = kFoldBuckets;
+  for (uint32_t b = b0; b < b1; ++b)
+    if (a.cnt[b]) {
+      best[t] = b;
+      break;
+    }
+  __syncthreads();
+  for (uint32_t d = 512; d > 0; d >>= 1) {
+    if (t < d) best[t] = min(best[t], best[t + d]);
+    __syncthreads();
+  }
+  const uint32_t kmax = (uint32_t)best[0];
+  const uint64_t max_blocks = kmax < kFoldBuckets ? fold_bucket_blocks(kFoldBuckets - 1 - kmax) : 0;
+  __syncthreads();
+  // each thread: the best cut at its buckets' boundaries, packed (cost, key)
+  uint32_t run = part[t] - s;
+  uint64_t brun = blk[t] - bl;
+  uint64_t mine = ~0ull;
+  uint32_t mine_h = 0;
+  for (uint32_t b = b0; b < b1; ++b) {  // cut before bucket b: h = run, its longest = bucket b
+    const uint32_t c = a.cnt[b];
+    if (c && a.head_cap) {
+      const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, fold_bucket_blocks(kFoldBuckets - 1 - b));
+      const uint64_t key = (min(cost, kCostMax) << 20) | b;
+      if (key < mine) {
+        mine = key;
+        mine_h = run;
+      }
+    }
+    a.cnt[b] = run;
+    run += c;
+    brun += (uint64_t)c * fold_bucket_blocks(kFoldBuckets - 1 - b);
+  }
+  if (t == 1023 && a.head_cap) {  // the cut after the last bucket: every lane on the head
+    const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, 0);
+    const uint64_t key = (min(cost, kCostMax) << 20) | kFoldBuckets;
+    if (key < mine) {
+      mine = key;
+      mine_h = run;
+    }
+  }
+  best[t] = mine;
+  part[t] = mine_h;
+  __syncthreads();
+  for (uint32_t d = 512; d > 0; d >>= 1) {
+    if (t < d && best[t + d] < best[t]) {
+      best[t] = best[t + d];
+      part[t] = part[t + d];
+    }
+    __syncthreads();
+  }
+  if (t == 0) {
+    a.info[0] = lanes;
+    a.info[1] = best[0] == ~0ull ? 0u : part[0];
+  }
+}
+
+// Each lane's rank inside its tile's key (LDS atomic), the tile's base in
+// each bucket (one global atomic per key present), order[base + rank] = i.
+__global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
+  __shared__ uint32_t hist[kFoldBuckets];  // counts, then the tile's bucket bases
+  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x) hist[j] = 0;
+  __syncthreads();
+  const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
+  uint32_t item[kFoldItems];  // key << 12 | rank (rank < kFoldTile = 4096), or kEmptyKey
+#pragma unroll
+  for (uint32_t r = 0; r < kFoldItems; ++r) {
+    const uint64_t i = base + r * 256 + threadIdx.x;
+    item[r] = kEmptyKey;
+    if (i < a.n && (!a.table || a.rep[i] == (uint32_t)i)) {
+      const uint32_t k = fold_key(a.len[i]);
+      item[r] = (k << 12) | atomicAdd(&hist[k], 1u);
+    }
+  }
+  __syncthreads();
+  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
+    if (hist[j]) hist[j] = atomicAdd(&a.cnt[j], hist[j]);
+  __syncthreads();
+#pragma unroll
+  for (uint32_t r = 0; r < kFoldItems; ++r) {
+    if (item[r] == kEmptyKey) continue;
+    a.order[hist[item[r] >> 12] + (item[r] & 0xFFFu)] = (uint32_t)(base + r * 256 + threadIdx.x);
+  }
+}
+
+__global__ __launch_bounds__(256) void k_fold_fill(const uint32_t* __restrict__ rep, uint64_t n,
+                                                   uint8_t* __restrict__ out) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint32_t r = rep[i];
+  if (r == (uint32_t)i) return;
+  const uint4* src = reinterpret_cast<const uint4*>(out + 32 * (uint64_t)r);
+  uint4* dst = reinterpret_cast<uint4*>(out + 32 * i);
+  dst[0] = src[0];
+  dst[1] = src[1];
+}
+
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
+  if (a.table) {
+    hipLaunchKernelGGL(k_fold_tilemax, dim3(ptiles), dim3(256), 0, st, a);
+    hipLaunchKernelGGL(k_fold_tilescan, dim3(1), dim3(1024), 0, st, a, (uint64_t)ptiles);
+    hipLaunchKernelGGL(k_fold_insert, dim3(ptiles), dim3(256), 0, st, a);
+  }
+  const unsigned ftiles = (unsigned)((a.n + kFoldTile - 1) / kFoldTile);
+  hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, a);
+  hipLaunchKernelGGL(k_fold_scatter, dim3(ftiles), dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st) {
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fold_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rep, n, out);
   return hipGetLastError();
 }
 

@@ -221,6 +221,14 @@ class Engine:
                                                        None if order is None else order.data_ptr(),
                                                        off.numel(), out.data_ptr(), self._stream_ptr(stream)))
 
+    def digest_batch_device_planned(self, arena, off, length, out, stream=None, fold: bool = False) -> None:
+        """msha_digest_batch_device_planned: lane order (and, with fold, alias
+        folding) planned on the GPU inside the call's launches."""
+        self._check(self._lib.msha_digest_batch_device_planned(self._ctx, arena.data_ptr(), off.data_ptr(),
+                                                               length.data_ptr(), off.numel(),
+                                                               1 if fold else 0, out.data_ptr(),
+                                                               self._stream_ptr(stream)))
+
     def digest_uniform_device(self, arena, stride: int, msg_len: int, n: int, out, stream=None) -> None:
         self._check(self._lib.msha_digest_uniform_device(self._ctx, arena.data_ptr(), stride, msg_len, n,
                                                          out.data_ptr(), self._stream_ptr(stream)))

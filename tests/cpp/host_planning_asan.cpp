@@ -20,7 +20,7 @@ namespace msha {
 bool plan_split(uint64_t, int, int, SplitPlan*, int) { return false; }
 hipError_t launch_digest_batch(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*,
                                const uint32_t*, uint64_t, uint8_t*, uint32_t*, int, int, hipStream_t,
-                               const SplitPlan*, LaunchKind*) {
+                               const SplitPlan*, LaunchKind*, const LaneGate*) {
   abort();
 }
 hipError_t launch_digest_uniform(const uint8_t*, uint64_t, uint64_t, uint64_t, uint8_t*, uint32_t*, int,
@@ -32,6 +32,9 @@ hipError_t launch_digest_of_digests(const uint8_t*, const uint32_t*, const uint6
   abort();
 }
 hipError_t launch_plan(const PlanArgs&, hipStream_t) { abort(); }
+hipError_t launch_fold_plan(const FoldArgs&, hipStream_t) { abort(); }
+hipError_t launch_fold_fill(const uint32_t*, uint64_t, uint8_t*, hipStream_t) { abort(); }
+bool uses_coop(uint64_t, int, int) { abort(); }
 }  // namespace msha
 
 static int failures = 0;

@@ -29,7 +29,7 @@ def test_exports_via_nm():
 
 
 def test_abi_version():
-    assert L.lib().msha_abi_version() == L.ABI_VERSION == 6
+    assert L.lib().msha_abi_version() == L.ABI_VERSION == 7
 
 
 def test_library_is_gfx950_code_object():
@@ -168,7 +168,7 @@ def test_stats_and_shard_stats_null_args():
     assert lib.msha_shard_count(None, ctypes.byref(n)) == L.MSHA_ERR_INVALID_ARG
     assert lib.msha_get_shard_stats(None, 0, None) == L.MSHA_ERR_INVALID_ARG
     assert ctypes.sizeof(L.MshaShardStats) == 8 * 15
-    assert ctypes.sizeof(L.MshaStats) == 8 * 19
+    assert ctypes.sizeof(L.MshaStats) == 8 * 20
 
 
 def _first_ref(off, ln):

@@ -1,0 +1,197 @@
+"""GPU parity of msha_digest_batch_device_planned: the device-resident batch
+whose lane order, alias folding and long-chain head are planned on the GPU
+(plan.hip k_fold_*), checked bit-exact against the oracle (OpenSSL leg, every
+distinct (off, len) hashed once) -- BASELINE config c5 at full size and per-rank
+slices, the head routing forced and disabled, every kernel policy, edge cases
+(one payload aliased n times, empty messages, messages past the exact block-
+count buckets) and seeded fuzz."""
+import numpy as np
+import pytest
+
+from mirbft_amd import MshaError
+from mirbft_amd import workloads as W
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(w):
+    import torch
+    dev = torch.device("cuda:0")
+    return (torch.from_numpy(w.arena).to(dev), torch.from_numpy(w.off.view(np.int64)).to(dev),
+            torch.from_numpy(w.len.view(np.int64)).to(dev))
+
+
+def _expect(w, threads=16):
+    if w.n == 0:
+        return np.zeros((0, 32), np.uint8)
+    key = np.stack([w.off, w.len], axis=1)
+    uniq, first, inv = np.unique(key, axis=0, return_index=True, return_inverse=True)
+    d = oracle.openssl_digest_batch(w.arena, w.off[first], w.len[first], threads)
+    return d[inv.reshape(-1)]
+
+
+def _run(engine, w, fold, stream=None):
+    import torch
+    d_arena, d_off, d_len = _dev(w)
+    out = torch.full((w.n, 32), 0xA5, dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device_planned(d_arena, d_off, d_len, out, stream=stream, fold=fold)
+    engine.device_status()
+    return out.cpu().numpy()
+
+
+def _delta(before, after, key):
+    return after[key] - before[key]
+
+
+@pytest.mark.parametrize("fold", [False, True])
+def test_c5_full_size_planned(engine, fold):
+    """BASELINE config c5 (2^23 mixed actions, aliased EpochChange pool) at full
+    size, the form bench.py times as c5_planned / c5_folded: every digest."""
+    import torch
+    w = W.c5_storm()
+    exp = _expect(w)
+    before = engine.stats()
+    got = _run(engine, w, fold)
+    after = engine.stats()
+    assert np.array_equal(got, exp)
+    assert _delta(before, after, "planned_device_calls") == 1
+    assert _delta(before, after, "launches_lane") == 1     # one lane launch over the whole order
+    torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+@pytest.mark.parametrize("fold", [False, True])
+def test_c5_rank_slice_routes_long_chains(engine, world, fold):
+    """A rank's slice of c5 over `world` GPUs: with folding, or at 8 GPUs, the
+    longest EpochChange chains outlast the lane kernel's share and run on the
+    cooperative kernel beside it (one coop + one lane launch); digests exact."""
+    w = W.c5_storm(n=(1 << 23) // world)
+    exp = _expect(w)
+    before = engine.stats()
+    got = _run(engine, w, fold)
+    after = engine.stats()
+    assert np.array_equal(got, exp)
+    if fold or world == 8:
+        assert _delta(before, after, "launches_coop") == 1
+    assert _delta(before, after, "launches_lane") == 1
+
+
+@pytest.mark.parametrize("pct", ["1", "100000"])
+def test_head_forced_and_empty(engine, monkeypatch, pct):
+    """Head threshold at 1 % of the balanced share (as many lanes as the
+    cooperative launch holds go to it) and at 1000x (no head at all)."""
+    monkeypatch.setenv("MSHA_PLAN_HEAD_PCT", pct)
+    w = W.c5_storm(n=1 << 18, first=12345)
+    exp = _expect(w)
+    for fold in (False, True):
+        assert np.array_equal(_run(engine, w, fold), exp)
+
+
+def test_head_disabled(engine, monkeypatch):
+    monkeypatch.setenv("MSHA_PLAN_HEAD", "0")
+    w = W.c5_storm(n=1 << 17)
+    before = engine.stats()
+    assert np.array_equal(_run(engine, w, True), _expect(w))
+    assert _delta(before, engine.stats(), "launches_coop") == 0
+
+
+@pytest.mark.parametrize("policy", ["lane", "coop"])
+def test_policies(engine, policy):
+    engine.set_kernel_policy(policy)
+    try:
+        w = W.c5_storm(n=1 << 16, first=777)
+        exp = _expect(w)
+        for fold in (False, True):
+            assert np.array_equal(_run(engine, w, fold), exp)
+    finally:
+        engine.set_kernel_policy("auto")
+
+
+@pytest.mark.parametrize("n", [1, 2, 63, 64, 65, 1000, 32768, 32769, 65536, 65537, 300_000])
+def test_one_payload_aliased(engine, n):
+    """n actions all naming one 5,000-byte payload: folded, one lane hashes it
+    and the fill copies its digest everywhere; unfolded, every lane hashes it."""
+    arena = W.random_bytes(W.SEED ^ 0x77, 0, 5000 + 64)
+    w = W.Workload("aliased", arena, np.zeros(n, np.uint64), np.full(n, 5000, np.uint64))
+    exp = np.tile(oracle.digest_batch(arena, np.zeros(1, np.uint64), np.full(1, 5000, np.uint64)), (n, 1))
+    assert np.array_equal(_run(engine, w, True), exp)
+    assert np.array_equal(_run(engine, w, False), exp)
+
+
+def test_empty_and_boundary_lengths(engine):
+    lens = np.array([0, 0, 1, 55, 56, 63, 64, 65, 119, 120, 0, 128, 4096 * 64 - 9, 4096 * 64,
+                     300_000, 1 << 20, 0] * 50, dtype=np.uint64)
+    off = np.zeros(lens.size, np.uint64)
+    off[1:] = np.cumsum((lens + np.uint64(15)) // np.uint64(16) * np.uint64(16))[:-1]
+    arena = W.random_bytes(W.SEED ^ 0x78, 0, int(off[-1] + lens[-1]) + 64)
+    w = W.Workload("boundary", arena, off, lens)
+    exp = _expect(w)
+    for fold in (False, True):
+        assert np.array_equal(_run(engine, w, fold), exp)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz(engine, seed):
+    """Random sizes (mostly small, a few up to 400 KB), aligned starts, packed /
+    aliased / reversed / overlapping-window layouts, folding on and off."""
+    rng = np.random.default_rng(4000 + seed)
+    n = int(rng.choice([1, 7, 100, 5000, 40_000, 120_000]))
+    ln = rng.integers(0, 2000, n).astype(np.uint64)
+    big = rng.random(n) < 0.005
+    ln[big] = rng.integers(10_000, 400_000, int(big.sum())).astype(np.uint64)
+    kind = int(rng.integers(0, 4))
+    steps = (ln + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    off = np.concatenate([[0], np.cumsum(steps)[:-1]]).astype(np.uint64)
+    size = int(off[-1] + ln[-1])
+    if kind == 1 and n > 1:                          # 30 % alias an earlier message
+        src = rng.integers(0, n, n)
+        al = (rng.random(n) < 0.3) & (src < np.arange(n))
+        off[al], ln[al] = off[src[al]], ln[src[al]]
+    elif kind == 2:                                  # reversed arena order
+        off = off[::-1].copy()
+        ln = ln[::-1].copy()
+    elif kind == 3:                                  # overlapping windows, 16-B aligned
+        size = int(ln.max()) + 8000
+        off = (rng.integers(0, 500, n) * 16).astype(np.uint64)
+    arena = W.random_bytes(W.SEED ^ (0x900 + seed), 0, size + 64)
+    w = W.Workload(f"fuzz{seed}", arena, off, ln)
+    exp = _expect(w, 8)
+    for fold in (False, True):
+        assert np.array_equal(_run(engine, w, fold), exp)
+
+
+def test_on_a_caller_stream(engine):
+    """Enqueued on the caller's stream (the head forked to the side stream and
+    joined back): the digests are complete once that stream is synchronized."""
+    import torch
+    s = torch.cuda.Stream()
+    w = W.c5_storm(n=1 << 20, first=99)
+    d_arena, d_off, d_len = _dev(w)
+    out = torch.zeros((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device_planned(d_arena, d_off, d_len, out, stream=s, fold=True)
+    s.synchronize()
+    assert np.array_equal(out.cpu().numpy(), _expect(w))
+    engine.device_status()
+
+
+def test_misaligned_flagged(engine):
+    import torch
+    arena = torch.zeros(4096, dtype=torch.uint8, device="cuda:0")
+    off = torch.tensor([0, 8, 16], dtype=torch.int64, device="cuda:0")
+    ln = torch.tensor([10, 10, 10], dtype=torch.int64, device="cuda:0")
+    out = torch.full((3, 32), 0xAB, dtype=torch.uint8, device="cuda:0")
+    engine.digest_batch_device_planned(arena, off, ln, out, fold=True)
+    with pytest.raises(MshaError):
+        engine.device_status()
+    assert (out[1] == 0).all()
+
+
+def test_bad_flags(engine):
+    import torch
+    from mirbft_amd import _lib as L
+    t = torch.zeros(64, dtype=torch.uint8, device="cuda:0")
+    o = torch.zeros(1, dtype=torch.int64, device="cuda:0")
+    rc = L.lib().msha_digest_batch_device_planned(engine._ctx, t.data_ptr(), o.data_ptr(), o.data_ptr(), 1,
+                                                  2, t.data_ptr(), None)
+    assert rc == L.MSHA_ERR_INVALID_ARG

@@ -95,6 +95,12 @@ def test_bench_two_ranks_on_the_engine():
     c5 = d["extra_configs"]["c5"]
     assert c5["n_gpus"] == 2 and c5["scaling"] == "strong" and c5["value"] > 0 and 0 < c5["frac"] < 1
     assert c5["blocks"] > 0 and "512 digests per rank" in c5["verified"]
+    # ... and its GPU-planned forms (every action hashed; aliases folded)
+    for form in ("c5_planned", "c5_folded"):
+        f = d["extra_configs"][form]
+        assert f["n_gpus"] == 2 and f["scaling"] == "strong" and f["value"] > 0 and f["blocks"] == c5["blocks"]
+        assert "512 digests per rank" in f["verified"] and f["kernel"] == "lane+coop"
+    assert d["extra_configs"]["c5_folded"]["hashed_blocks"] < c5["blocks"] == d["extra_configs"]["c5_planned"]["hashed_blocks"]
     # the CPU baseline at N > 1 too (rank 0, after the ranks released their GPUs)
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0 and cb["impl"]
