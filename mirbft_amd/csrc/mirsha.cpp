@@ -239,7 +239,8 @@ struct Device {
   // long chains runs on side_stream, forked from and joined to the caller's
   DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_info;
   hipStream_t side_stream = nullptr;
-  hipEvent_t ev_fork = nullptr, ev_fplan = nullptr, ev_join = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_fplan = nullptr, ev_join = nullptr, ev_fdone = nullptr;
+  bool fdone_recorded = false;  // ev_fdone: the last planned call's work is queued behind it
   // per-call shard description
   uint64_t lo = 0, hi = 0;        // message/action range
   uint64_t arena_bytes = 0;       // staged arena size (without slack)
@@ -265,7 +266,7 @@ struct Device {
     for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1], &sm_stage, &sm_res, &h_gmap, &h_small, &h_rep})
       b->release();
     for (hipEvent_t* e : {&ev0, &ev1, &ev_up0, &ev_up1, &ev_k0, &ev_meta, &ev_plan, &ev_p0, &ev_p1, &slot_free[0],
-                          &slot_free[1], &chunk_in, &ev_fork, &ev_fplan, &ev_join}) {
+                          &slot_free[1], &chunk_in, &ev_fork, &ev_fplan, &ev_join, &ev_fdone}) {
       if (*e) (void)hipEventDestroy(*e);
       *e = nullptr;
     }
@@ -2528,6 +2529,10 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // resident before the lane kernel fills every SIMD (queued the other way
     // round, the head could not get a CU's registers until the lane kernel
     // drained: c5 folded 6.2 ms, its 1,427-block chain starting at the end).
+    // The planner's scratch (table, order, counters) is the context's: a call
+    // on another stream must not overwrite it while an earlier call still reads it.
+    if (!d.ev_fdone) HIPCHK(hipEventCreateWithFlags(&d.ev_fdone, hipEventDisableTiming));
+    if (d.fdone_recorded) HIPCHK(hipStreamWaitEvent(st, d.ev_fdone, 0));
     hipStream_t ps = st;
     if (head) {
       if (!d.side_stream) HIPCHK(hipStreamCreateWithFlags(&d.side_stream, hipStreamNonBlocking));
@@ -2582,6 +2587,8 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       if (head) HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
     }
     if (fold) HIPCHK(msha::launch_fold_fill(fa.rep, n, d_out, st));
+    HIPCHK(hipEventRecord(d.ev_fdone, st));
+    d.fdone_recorded = true;
     ctx->stats.planned_device_calls++;
     if (trace_on()) {  // MSHA_TRACE: the GPU's plan (waits for the call)
       uint32_t info[2] = {0, 0};

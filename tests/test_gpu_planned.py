@@ -65,7 +65,9 @@ def test_c5_full_size_planned(engine, fold):
 def test_c5_rank_slice_routes_long_chains(engine, world, fold):
     """A rank's slice of c5 over `world` GPUs: with folding, or at 8 GPUs, the
     longest EpochChange chains outlast the lane kernel's share and run on the
-    cooperative kernel beside it (one coop + one lane launch); digests exact."""
+    cooperative kernel beside it (the head launch is queued whenever the batch
+    is above the cooperative range; its size is decided on the GPU, MSHA_TRACE
+    prints it); digests exact."""
     w = W.c5_storm(n=(1 << 23) // world)
     exp = _expect(w)
     before = engine.stats()
@@ -79,8 +81,8 @@ def test_c5_rank_slice_routes_long_chains(engine, world, fold):
 
 @pytest.mark.parametrize("pct", ["1", "100000"])
 def test_head_forced_and_empty(engine, monkeypatch, pct):
-    """Head threshold at 1 % of the balanced share (as many lanes as the
-    cooperative launch holds go to it) and at 1000x (no head at all)."""
+    """The head's cost term in the GPU planner's cut scaled to 1 % (a nearly
+    free head: the cut takes as many lanes as pays) and to 1000x (no head)."""
     monkeypatch.setenv("MSHA_PLAN_HEAD_PCT", pct)
     w = W.c5_storm(n=1 << 18, first=12345)
     exp = _expect(w)
@@ -173,6 +175,26 @@ def test_on_a_caller_stream(engine):
     s.synchronize()
     assert np.array_equal(out.cpu().numpy(), _expect(w))
     engine.device_status()
+
+
+def test_calls_on_two_streams(engine):
+    """Back-to-back planned calls on two streams share the context's planner
+    scratch: the second waits for the first (ev_fdone), both digest sets exact."""
+    import torch
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    w1 = W.c5_storm(n=1 << 19, first=5)
+    w2 = W.c5_storm(n=(1 << 18) + 77, first=1 << 22)
+    a1, o1, l1 = _dev(w1)
+    a2, o2, l2 = _dev(w2)
+    out1 = torch.zeros((w1.n, 32), dtype=torch.uint8, device="cuda:0")
+    out2 = torch.zeros((w2.n, 32), dtype=torch.uint8, device="cuda:0")
+    for _ in range(3):
+        engine.digest_batch_device_planned(a1, o1, l1, out1, stream=s1, fold=True)
+        engine.digest_batch_device_planned(a2, o2, l2, out2, stream=s2, fold=False)
+    torch.cuda.synchronize()
+    engine.device_status()
+    assert np.array_equal(out1.cpu().numpy(), _expect(w1))
+    assert np.array_equal(out2.cpu().numpy(), _expect(w2))
 
 
 def test_misaligned_flagged(engine):
