@@ -78,3 +78,20 @@ def test_host_api_leg_failure_is_reported_not_fatal(monkeypatch):
     assert seen["cmd"][2:] == ["--mode", "lib", "--config", "c5", "--gpus", "1", "--steps", "5", "--warmup", "2"]
     assert "WORLD_SIZE" not in seen["env"] and "MASTER_PORT" not in seen["env"]
     assert seen["env"]["MSHA_VIRTUAL_SHARDS"] == "2"
+
+
+def test_c5_forms_share_the_workload_and_count_hashed_blocks():
+    """The three c5 forms build the same storm slice; only c5_folded's hashed
+    blocks (its roofline numerator) drop: each distinct (off, len) once."""
+    sys.path.insert(0, ROOT)
+    import bench
+    import numpy as np
+    assert set(bench.C5_FORMS) == set(bench.C5_FORM_NOTES)
+    w = bench.build_workload("c5_folded", 3, 64)        # 2^17 actions of the node's storm
+    w2 = bench.build_workload("c5", 3, 64)
+    assert np.array_equal(w.off, w2.off) and np.array_equal(w.len, w2.len)
+    assert bench.hashed_blocks(w, "c5") == bench.hashed_blocks(w, "c5_planned") == w.blocks
+    key = np.unique(np.stack([w.off, w.len], axis=1), axis=0)
+    L = key[:, 1]
+    exp = int(((L >> np.uint64(6)) + np.where((L & np.uint64(63)) < 56, 1, 2).astype(np.uint64)).sum())
+    assert bench.hashed_blocks(w, "c5_folded") == exp < w.blocks
