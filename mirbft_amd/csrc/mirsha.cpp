@@ -2522,6 +2522,10 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       d.f_rep.ensure(4 * n);
       d.f_tmax.ensure(8 * ((n + 4095) / 4096));
     }
+    // The planner's scratch (table, order, counters) is the context's: a call
+    // on another stream must not overwrite it while an earlier call still reads it.
+    if (!d.ev_fdone) HIPCHK(hipEventCreateWithFlags(&d.ev_fdone, hipEventDisableTiming));
+    if (d.fdone_recorded) HIPCHK(hipStreamWaitEvent(st, d.ev_fdone, 0));
     // With a head, the planner and then the head's cooperative launch run on
     // the side stream, and the lane kernel on `stream` waits for the planner's
     // event: the head's packet follows the planner in its own queue while the
@@ -2529,10 +2533,6 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // resident before the lane kernel fills every SIMD (queued the other way
     // round, the head could not get a CU's registers until the lane kernel
     // drained: c5 folded 6.2 ms, its 1,427-block chain starting at the end).
-    // The planner's scratch (table, order, counters) is the context's: a call
-    // on another stream must not overwrite it while an earlier call still reads it.
-    if (!d.ev_fdone) HIPCHK(hipEventCreateWithFlags(&d.ev_fdone, hipEventDisableTiming));
-    if (d.fdone_recorded) HIPCHK(hipStreamWaitEvent(st, d.ev_fdone, 0));
     hipStream_t ps = st;
     if (head) {
       if (!d.side_stream) HIPCHK(hipStreamCreateWithFlags(&d.side_stream, hipStreamNonBlocking));
