@@ -513,8 +513,13 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     __syncthreads();
   }
   if (t == 0) {
+    // The head's last workgroup has room to spare (a workgroup runs as long as
+    // its longest chain): fill it with the next-longest lanes, which would
+    // otherwise run as lone chains on the lane kernel (folded c5: 37 -> 128).
+    const uint32_t h = best[0] == ~0ull ? 0u : part[0];
+    const uint32_t hfill = (h + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg * kCoopMsgsPerWg;
     a.info[0] = lanes;
-    a.info[1] = best[0] == ~0ull ? 0u : part[0];
+    a.info[1] = min(min(hfill, lanes), a.head_cap);
   }
 }
 
