@@ -858,6 +858,134 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
   }
 }
 
+// ---------------------------------------------------------------------------
+// The planned launch's head of long chains (msha_digest_batch_device_planned):
+// what bounds it is one chain's latency, and the cooperative consumer is
+// issue-bound at 14 VALU instructions a round. Here TWO lanes carry a message:
+// lane p < 8 of each 16-lane row the e-side (e f g h), lane 15 - p the a-side
+// (a b c d). One v_alignbit x3 + xor3 then computes Sigma1 in the e-lane and
+// Sigma0 in the a-lane (per-lane rotate amounts), Ch and Maj are one bitop3
+// each, and the two new words come from two row_mirror DPP adds that write only
+// their side's lanes (bank_mask) -- 11 instructions a round:
+//   e-lane  U = Sig1 + Ch + (h + KW) = T1,   e' = mirror(d) + T1
+//   a-lane  T = Sig0 + Maj (its KW is 0) = T2, a' = mirror(T1) + T2
+// Register-resident, one wave alone on its SIMD: 21.1 against 23.7 ns a round
+// (tools/chain_dpp_microbench.hip, profiles/r03_chain_dpp/). Workgroup = one
+// producer wave (64 messages: loads, padding, K+W schedules into LDS, as in
+// k_digest_coop) and two consumer waves of 32 messages; EXCL as above (the
+// head's CUs hold nothing else); each lane stores its side's four digest words.
+// ---------------------------------------------------------------------------
+#define MSHA_DROUND(X, Y, Z, W, kw)                                                              \
+  {                                                                                              \
+    const uint32_t s_ = xor3(__builtin_amdgcn_alignbit(X, X, sh1), __builtin_amdgcn_alignbit(X, X, sh2), \
+                             __builtin_amdgcn_alignbit(X, X, sh3));                              \
+    const uint32_t u_ = s_ + ch(X, Y, Z) + (W + (kw));                                           \
+    uint32_t t_ = s_ + maj(X, Y, Z) + (kw);                                                      \
+    asm volatile("v_add_u32_dpp %0, %1, %2 row_mirror row_mask:0xf bank_mask:0x3"                \
+                 : "+v"(t_) : "v"(W), "v"(u_));                                                  \
+    asm volatile("v_add_u32_dpp %0, %1, %0 row_mirror row_mask:0xf bank_mask:0xc"                \
+                 : "+v"(t_) : "v"(u_));                                                          \
+    W = t_;                                                                                      \
+  }
+#define MSHA_D4(q)                                 \
+  {                                                \
+    const uint4 v_ = kv[q];                        \
+    MSHA_DROUND(X, Y, Z, W, v_.x)                  \
+    MSHA_DROUND(W, X, Y, Z, v_.y)                  \
+    MSHA_DROUND(Z, W, X, Y, v_.z)                  \
+    MSHA_DROUND(Y, Z, W, X, v_.w)                  \
+  }
+
+template <int MODE>
+__global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint64_t* __restrict__ len,
+                                                       const uint32_t* __restrict__ order,
+                                                       uint64_t n, uint8_t* __restrict__ out,
+                                                       uint32_t* __restrict__ err,
+                                                       const uint32_t* __restrict__ limit) {
+  // [slot][quad t/4][message] x 16 B, then 16 zero quads (the a-lanes' K+W)
+  __shared__ uint4 kw[2][kCoopSlotQuads * 64 + kCoopSlotQuads];
+  __shared__ uint32_t s_nb;
+  asm volatile("" ::: "v255", "a255");  // exclusive CU (see k_digest_coop EXCL)
+  __builtin_amdgcn_s_setprio(3);
+  const unsigned lane = threadIdx.x & 63;
+  const unsigned wave = threadIdx.x >> 6;
+  const bool producer = wave == 0;
+  const unsigned p = lane & 15;
+  const bool eside = p < 8;
+  // message of this lane inside the workgroup
+  const unsigned msg = producer ? lane : (wave - 1) * 32 + (lane >> 4) * 8 + (eside ? p : 15 - p);
+  const uint64_t i = (uint64_t)blockIdx.x * kChain2MsgsPerWg + msg;
+  bool active = i < n && i < *limit;
+  uint64_t m = 0;
+  if (active) {
+    const uint32_t v = order[i];
+    active = v != kNoLane;
+    m = active ? v : 0;
+  }
+  const uint8_t* pa = arena;
+  uint64_t L = 0;
+  if (active) {
+    pa = arena + off[m];
+    L = len[m];
+    if (reinterpret_cast<uintptr_t>(pa) & 15) {
+      active = false;
+      L = 0;
+      if (!producer && eside) check_aligned(pa, out + 32 * m, err);
+    }
+  }
+  const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
+  const uint32_t nb = nfull + (r < 56 ? 1 : 2);
+  if (threadIdx.x == 0) s_nb = 0;
+  if (threadIdx.x < 2 * kCoopSlotQuads) kw[threadIdx.x >> 4][kCoopSlotQuads * 64 + (threadIdx.x & 15)] =
+      make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  if (producer && active) atomicMax(&s_nb, nb);
+  __syncthreads();
+  const uint32_t NB = s_nb;
+  if (producer) {
+    uint32_t raw[16], w[16];
+    if (active) load_block16<MODE>(pa, raw);
+    for (uint32_t b = 0; b < NB; ++b) {
+      if (b < nfull) {
+        to_words(raw, w);
+      } else if (b == nfull) {
+        uint32_t rr = r;
+        asm volatile("" : "+v"(rr));
+        build_tail(raw, rr, L, w);
+      } else {
+        length_block(L, w);
+      }
+      if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
+      schedule_kw(w, &kw[b & 1][lane]);
+      __syncthreads();
+    }
+  } else {
+    // e-side: e f g h, rotates 6 11 25; a-side: a b c d, rotates 2 13 22
+    uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
+    uint32_t H2 = eside ? 0x1f83d9abu : 0x3c6ef372u, H3 = eside ? 0x5be0cd19u : 0xa54ff53au;
+    const uint32_t sh1 = eside ? 6 : 2, sh2 = eside ? 11 : 13, sh3 = eside ? 25 : 22;
+    const unsigned col = eside ? msg : kCoopSlotQuads * 64;  // a-lanes read the zero quads
+    const unsigned qstride = eside ? 64 : 1;
+    for (uint32_t b = 0; b < NB; ++b) {
+      __syncthreads();
+      uint4 kv[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) kv[q] = kw[b & 1][col + q * qstride];
+      uint32_t X = H0, Y = H1, Z = H2, W = H3;
+      MSHA_D4(0) MSHA_D4(1) MSHA_D4(2) MSHA_D4(3) MSHA_D4(4) MSHA_D4(5) MSHA_D4(6) MSHA_D4(7)
+      MSHA_D4(8) MSHA_D4(9) MSHA_D4(10) MSHA_D4(11) MSHA_D4(12) MSHA_D4(13) MSHA_D4(14) MSHA_D4(15)
+      H0 += X; H1 += Y; H2 += Z; H3 += W;
+      if (active && b + 1 == nb)
+        *reinterpret_cast<uint4*>(out + 32 * m + (eside ? 16 : 0)) =
+            make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));
+    }
+  }
+}
+#undef MSHA_D4
+#undef MSHA_DROUND
+
 // Uniform layout: message i is arena[i*stride : i*stride + msg_len].
 template <int MODE>
 __global__ __launch_bounds__(256, 8) void k_digest_uniform(const uint8_t* __restrict__ arena,
@@ -997,10 +1125,16 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
   set_kind(kind, kLaunchNone);
   if (n == 0) return hipSuccess;
   const uint32_t* head = gate ? gate->head : nullptr;
-  if (gate && gate->head_part) {  // the planned launch's long chains: cooperative, up to *head
-    const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
-    hipLaunchKernelGGL((k_digest_coop<kPrefetch, true>), dim3(grid), dim3(256), kCoopDynLds, st, arena, off,
-                       len, order, out_idx, n, out, err, head);
+  if (gate && gate->head_part) {  // the planned launch's long chains, up to *head
+    if (gate->two_lane && order && !out_idx) {
+      const unsigned grid = (unsigned)((n + kChain2MsgsPerWg - 1) / kChain2MsgsPerWg);
+      hipLaunchKernelGGL(k_digest_chain2<kPrefetch>, dim3(grid), dim3(192), 0, st, arena, off, len, order, n,
+                         out, err, head);
+    } else {
+      const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
+      hipLaunchKernelGGL((k_digest_coop<kPrefetch, true>), dim3(grid), dim3(256), kCoopDynLds, st, arena, off,
+                         len, order, out_idx, n, out, err, head);
+    }
     set_kind(kind, kLaunchCoop);
     return hipGetLastError();
   }

@@ -45,6 +45,7 @@ constexpr uint32_t kNoLane = 0xFFFFFFFFu;
 struct LaneGate {
   const uint32_t* head = nullptr;
   bool head_part = false;
+  bool two_lane = false;  // head_part: k_digest_chain2 instead of the cooperative kernel
 };
 
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
@@ -54,8 +55,10 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
                                const LaneGate* gate = nullptr);
 // Does launch_digest_batch use cooperative chaining for an n-message launch?
 bool uses_coop(uint64_t n, int cus, int policy);
-// Messages per workgroup of the cooperative kernel (one workgroup per CU).
+// Messages per workgroup of the cooperative kernel (one workgroup per CU) and
+// of the two-lane head chain (k_digest_chain2).
 constexpr unsigned kCoopMsgsPerWg = 128;
+constexpr unsigned kChain2MsgsPerWg = 64;
 hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st, LaunchKind* kind = nullptr);
@@ -129,6 +132,7 @@ struct FoldArgs {
   uint32_t lane_cycles = 7000;
   uint32_t coop_cycles = 4200;
   uint32_t head_pct = 100;
+  uint32_t head_per_wg = 128;    // messages per head workgroup (one CU each)
 };
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st);
 // out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.

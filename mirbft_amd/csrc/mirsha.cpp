@@ -2557,7 +2557,17 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.order = d.f_order.as<uint32_t>();
     fa.info = d.f_info.as<uint32_t>();
     fa.simds = (uint32_t)d.cus * 4;
-    fa.head_cap = head ? (uint32_t)std::min<uint64_t>(n, (uint64_t)d.cus * msha::kCoopMsgsPerWg) : 0;
+    // The head's kernel. Folded, a head is the few distinct long payloads: the
+    // two-lane chain (k_digest_chain2, 64 messages per CU, ~10 % fewer cycles a
+    // block) shortens it. Unfolded, a storm's head can be thousands of chains
+    // (19,456 over 8 GPUs): the cooperative kernel holds twice as many per CU,
+    // and the two-lane one made that case 3.0 -> 4.2 ms (profiles/r03_chain_dpp/).
+    // MSHA_HEAD_CHAIN2: 0 never, 2 always (A/B).
+    const uint64_t chain2_env = env_u64("MSHA_HEAD_CHAIN2", 1);
+    const bool two_lane = chain2_env == 2 || (chain2_env == 1 && fold);
+    fa.head_per_wg = two_lane ? msha::kChain2MsgsPerWg : msha::kCoopMsgsPerWg;
+    fa.head_cap = head ? (uint32_t)std::min<uint64_t>(n, (uint64_t)d.cus * fa.head_per_wg) : 0;
+    fa.coop_cycles = two_lane ? 3800 : 4200;
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     HIPCHK(msha::launch_fold_plan(fa, ps));
     const uint32_t* order = d.f_order.as<uint32_t>();
@@ -2574,6 +2584,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
         msha::LaneGate hg;
         hg.head = fa.info + 1;
         hg.head_part = true;
+        hg.two_lane = two_lane;
         HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, order, nullptr, fa.head_cap, d_out,
                                          d.err.as<uint32_t>(), d.cus, MSHA_KERNEL_COOP, d.side_stream, nullptr,
                                          &kind, &hg));

@@ -424,7 +424,7 @@ __global__ __launch_bounds__(256) void k_fold_keys(FoldArgs a) {
 // the head's term (A/B: 1 = a nearly free head, large = none).
 __device__ __forceinline__ uint64_t head_cost(const FoldArgs& a, uint64_t h, uint64_t bh, uint64_t btot,
                                               uint64_t max_blocks, uint64_t next_blocks) {
-  const uint64_t cus = a.simds / 4, hcus = (h + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg;
+  const uint64_t cus = a.simds / 4, hcus = (h + a.head_per_wg - 1) / a.head_per_wg;
   if (h > a.head_cap || hcus >= cus) return ~0ull;
   const uint64_t t_head = h ? max_blocks * a.coop_cycles / 100 * a.head_pct : 0;
   const uint64_t t_body = (btot - bh) * a.wave_block_cycles / (64ull * 4 * (cus - hcus));
@@ -517,7 +517,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     // its longest chain): fill it with the next-longest lanes, which would
     // otherwise run as lone chains on the lane kernel (folded c5: 37 -> 128).
     const uint32_t h = best[0] == ~0ull ? 0u : part[0];
-    const uint32_t hfill = (h + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg * kCoopMsgsPerWg;
+    const uint32_t hfill = (h + a.head_per_wg - 1) / a.head_per_wg * a.head_per_wg;
     a.info[0] = lanes;
     a.info[1] = min(min(hfill, lanes), a.head_cap);
   }

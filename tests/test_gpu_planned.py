@@ -90,6 +90,20 @@ def test_head_forced_and_empty(engine, monkeypatch, pct):
         assert np.array_equal(_run(engine, w, fold), exp)
 
 
+@pytest.mark.parametrize("chain2", ["0", "2"])
+def test_head_kernel_either_way(engine, monkeypatch, chain2):
+    """The head runs on the two-lane chain kernel (k_digest_chain2: folded calls
+    by default) or the cooperative one (unfolded by default); force each the
+    other way, with a large head (cost scaled down) and the default one."""
+    monkeypatch.setenv("MSHA_HEAD_CHAIN2", chain2)
+    w = W.c5_storm(n=1 << 17, first=4242)
+    exp = _expect(w)
+    for pct in ("1", "100"):
+        monkeypatch.setenv("MSHA_PLAN_HEAD_PCT", pct)
+        for fold in (False, True):
+            assert np.array_equal(_run(engine, w, fold), exp)
+
+
 def test_head_disabled(engine, monkeypatch):
     monkeypatch.setenv("MSHA_PLAN_HEAD", "0")
     w = W.c5_storm(n=1 << 17)
