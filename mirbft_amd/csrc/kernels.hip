@@ -896,19 +896,24 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
     MSHA_DROUND(Y, Z, W, X, v_.w)                  \
   }
 
-template <int MODE>
+// Also AUTO's kernel for launches of at most 64 messages per CU (a call of a
+// few actions at low load: one chain's latency is the call's), where every
+// workgroup gets a CU of its own: EXCL false there. order, out_idx and limit
+// may be null (identity, slot = message, no device-side limit).
+template <int MODE, bool EXCL>
 __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ off,
                                                        const uint64_t* __restrict__ len,
                                                        const uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ out_idx,
                                                        uint64_t n, uint8_t* __restrict__ out,
                                                        uint32_t* __restrict__ err,
                                                        const uint32_t* __restrict__ limit) {
   // [slot][quad t/4][message] x 16 B, then 16 zero quads (the a-lanes' K+W)
   __shared__ uint4 kw[2][kCoopSlotQuads * 64 + kCoopSlotQuads];
   __shared__ uint32_t s_nb;
-  asm volatile("" ::: "v255", "a255");  // exclusive CU (see k_digest_coop EXCL)
-  __builtin_amdgcn_s_setprio(3);
+  if (EXCL) asm volatile("" ::: "v255", "a255");  // exclusive CU (see k_digest_coop EXCL)
+  if (EXCL) __builtin_amdgcn_s_setprio(3);
   const unsigned lane = threadIdx.x & 63;
   const unsigned wave = threadIdx.x >> 6;
   const bool producer = wave == 0;
@@ -917,13 +922,16 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   // message of this lane inside the workgroup
   const unsigned msg = producer ? lane : (wave - 1) * 32 + (lane >> 4) * 8 + (eside ? p : 15 - p);
   const uint64_t i = (uint64_t)blockIdx.x * kChain2MsgsPerWg + msg;
-  bool active = i < n && i < *limit;
-  uint64_t m = 0;
-  if (active) {
+  bool active = i < n && (!limit || i < *limit);
+  uint64_t m = i;  // metadata index
+  if (active && order) {
     const uint32_t v = order[i];
     active = v != kNoLane;
-    m = active ? v : 0;
+    m = v;
   }
+  uint64_t o = m;  // digest slot
+  if (active && out_idx) o = out_idx[i];
+  if (!active) m = o = 0;
   const uint8_t* pa = arena;
   uint64_t L = 0;
   if (active) {
@@ -932,7 +940,7 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     if (reinterpret_cast<uintptr_t>(pa) & 15) {
       active = false;
       L = 0;
-      if (!producer && eside) check_aligned(pa, out + 32 * m, err);
+      if (!producer && eside) check_aligned(pa, out + 32 * o, err);
     }
   }
   const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
@@ -978,7 +986,7 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
       MSHA_D4(8) MSHA_D4(9) MSHA_D4(10) MSHA_D4(11) MSHA_D4(12) MSHA_D4(13) MSHA_D4(14) MSHA_D4(15)
       H0 += X; H1 += Y; H2 += Z; H3 += W;
       if (active && b + 1 == nb)
-        *reinterpret_cast<uint4*>(out + 32 * m + (eside ? 16 : 0)) =
+        *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =
             make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));
     }
   }
@@ -1126,10 +1134,10 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
   if (n == 0) return hipSuccess;
   const uint32_t* head = gate ? gate->head : nullptr;
   if (gate && gate->head_part) {  // the planned launch's long chains, up to *head
-    if (gate->two_lane && order && !out_idx) {
+    if (gate->two_lane) {
       const unsigned grid = (unsigned)((n + kChain2MsgsPerWg - 1) / kChain2MsgsPerWg);
-      hipLaunchKernelGGL(k_digest_chain2<kPrefetch>, dim3(grid), dim3(192), 0, st, arena, off, len, order, n,
-                         out, err, head);
+      hipLaunchKernelGGL((k_digest_chain2<kPrefetch, true>), dim3(grid), dim3(192), 0, st, arena, off, len,
+                         order, out_idx, n, out, err, head);
     } else {
       const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
       hipLaunchKernelGGL((k_digest_coop<kPrefetch, true>), dim3(grid), dim3(256), kCoopDynLds, st, arena, off,
@@ -1149,6 +1157,16 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
     return hipGetLastError();
   }
   if (uses_coop(n, cus, policy) && !head) {
+    if (policy == 0 && n <= (uint64_t)cus * kChain2MsgsPerWg && env_int("MSHA_SMALL_CHAIN2", 1)) {
+      // AUTO, at most 64 messages per CU: the two-lane chain, one workgroup per CU
+      // (64 KiB of dynamic LDS on top of its 33 KiB keeps a second one off the CU,
+      // whose consumers would share SIMDs with the first's)
+      const unsigned grid = (unsigned)((n + kChain2MsgsPerWg - 1) / kChain2MsgsPerWg);
+      hipLaunchKernelGGL((k_digest_chain2<kPrefetch, false>), dim3(grid), dim3(192), 64 * 1024, st, arena, off,
+                         len, order, out_idx, n, out, err, nullptr);
+      set_kind(kind, kLaunchCoop);
+      return hipGetLastError();
+    }
     const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
     hipLaunchKernelGGL(k_digest_coop<kPrefetch>, dim3(grid), dim3(256), kCoopDynLds, st, arena, off, len,
                        order, out_idx, n, out, err, nullptr);
