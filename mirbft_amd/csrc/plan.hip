@@ -380,13 +380,30 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   }
   const bool first_ever = blockIdx.x == 0 && threadIdx.x == 0;
   uint64_t run = max(a.tmax[blockIdx.x], threadIdx.x ? part[threadIdx.x - 1] : 0ull);
+  // Candidates are few (c5: 5 %) but spread over every wave: claiming them in
+  // place would run each wave's claim loop (a load -> CAS -> compare chain of
+  // memory round trips) once per item row. They go to an LDS list instead and
+  // the workgroup's threads claim them side by side.
+  __shared__ uint32_t cand[kPlanTile];
+  __shared__ uint32_t ncand;
+  if (threadIdx.x == 0) ncand = 0;
+  __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < kPlanItems; ++r) {
     const uint64_t i = base + r;
     if (i >= a.n) break;
     const bool fresh = o[r] > run || (first_ever && r == 0);  // above every earlier offset
-    a.rep[i] = fresh ? (uint32_t)i : fold_claim(a, i, o[r], a.len[i]);
+    if (fresh)
+      a.rep[i] = (uint32_t)i;
+    else
+      cand[atomicAdd(&ncand, 1u)] = (uint32_t)(i - (uint64_t)blockIdx.x * kPlanTile);
     run = max(run, o[r]);
+  }
+  __syncthreads();
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kPlanTile;
+  for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
+    const uint64_t i = tile0 + cand[c];
+    a.rep[i] = fold_claim(a, i, a.off[i], a.len[i]);
   }
 }
 
