@@ -123,13 +123,17 @@ struct FoldArgs {
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;
   // The head: the cut of the longest lanes that minimises the launch's
-  // estimated end (plan.hip head_cost). SIMD cycles per block, measured (c5
-  // slices, rocprofv3 timelines, profiles/r03_planned/): a lane-kernel wave
-  // among 8 per SIMD ~5,700 per wave-block; a long chain on the lane kernel
-  // ~7,000 (the oldest wave of its SIMD); on the cooperative kernel, alone on
-  // its CU at top priority, ~4,200. head_pct scales the head's term (A/B).
-  uint32_t wave_block_cycles = 5700;
-  uint32_t lane_cycles = 7000;
+  // estimated end (plan.hip head_cost), in SIMD cycles per block, measured (c5
+  // slices, rocprofv3 timelines, profiles/r03_planned/): the lane kernel's
+  // throughput on a storm's mixed lanes ~6,500 per wave-block (uniform batches:
+  // 5,700); a long chain on the lane kernel among loaded SIMDs ~8,000 (7,000 as
+  // the oldest wave of a lightly loaded one); on the cooperative consumer, alone
+  // on its CU at top priority, ~4,200 (the two-lane head ~3,800). A sweep of the
+  // first two (MSHA_PLAN_LANE_CYCLES / MSHA_PLAN_WAVE_CYCLES,
+  // profiles/r03_planned/calibration/): 8,000 / 6,500 ran c5 over 8 GPUs 3.00 ->
+  // 2.85 ms, equal at 2 and 4. head_pct scales the head's term (A/B).
+  uint32_t wave_block_cycles = 6500;
+  uint32_t lane_cycles = 8000;
   uint32_t coop_cycles = 4200;
   uint32_t head_pct = 100;
   uint32_t head_per_wg = 128;    // messages per head workgroup (one CU each)

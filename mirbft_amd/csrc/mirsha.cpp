@@ -2569,6 +2569,8 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.head_cap = head ? (uint32_t)std::min<uint64_t>(n, (uint64_t)d.cus * fa.head_per_wg) : 0;
     fa.coop_cycles = two_lane ? 3800 : 4200;
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
+    fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
+    fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);
     HIPCHK(msha::launch_fold_plan(fa, ps));
     const uint32_t* order = d.f_order.as<uint32_t>();
     msha::LaunchKind kind;
