@@ -145,6 +145,11 @@ def _time_cpu(fn, n: int, nbytes_per: int, seconds: float):
 
 
 CPU_THREADS = 16   # the GPU box's CPU share per GPU
+# cpu_baseline.kind names what `value` timed: OpenSSL's SHA-256 (SHA-NI) on one
+# thread when libcrypto loads -- a stand-in for Go's crypto/sha256, which cannot
+# run here -- else the oracle's scalar C port (always reported as scalar_port).
+OPENSSL_KIND = "openssl-sha-ni-1-thread (proxy for Go crypto/sha256)"
+SCALAR_KIND = "port"
 
 
 def cpu_baseline(w, seconds: float):
@@ -157,7 +162,7 @@ def cpu_baseline(w, seconds: float):
     off, ln = w.off[:n], w.len[:n]
     per = int(ln.sum())
     v, g, done, el = _time_cpu(lambda: oracle.digest_batch(w.arena, off, ln), n, per, seconds / 2)
-    line = {"value": None, "unit": "digests/s", "cores": 1, "kind": "port", "impl": None, "gbps": None,
+    line = {"value": None, "unit": "digests/s", "cores": 1, "kind": SCALAR_KIND, "impl": None, "gbps": None,
             "scalar_port": {"value": v, "gbps": g, "source": "oracle/sha256_oracle.c, plain scalar C, 1 thread"},
             "sample": f"first {n} messages of the same workload, repeated for {el:.1f} s "
                       f"({done} digests) per leg"}
@@ -170,7 +175,7 @@ def cpu_baseline(w, seconds: float):
         # value: the reference's loop (serial.go:180-198) on ONE core (its single hash
         # goroutine, mirbft.go:470) with the fastest SHA-256 this host has (OpenSSL,
         # SHA-NI): Go 1.15's AVX2 crypto/sha256 would be slower, the scalar port slower still
-        line["value"], line["gbps"] = v1, g1
+        line["value"], line["gbps"], line["kind"] = v1, g1, OPENSSL_KIND
         line["impl"] = ("openssl-sha-ni-1-thread (proxy for Go crypto/sha256): the oracle's restatement of "
                         "serial.go:180-198 in C over OpenSSL EVP SHA-256, oracle/sha256_openssl.c")
         m = min(w.n, 4096 * CPU_THREADS)
@@ -190,23 +195,37 @@ def cpu_baseline(w, seconds: float):
     return line
 
 
-PMC_FILE = "profiles/r02_pmc.json"          # tools/pmc_valu.sh -> tools/pmc_summary.py
-TRAFFIC_FILE = "profiles/r01_traffic.json"  # tools/pmc_traffic.sh (first collection)
+PMC_FILE = "profiles/r04_pmc.json"          # tools/pmc_valu.sh -> tools/pmc_summary.py, this round's code
 
 
 def measured_traffic(cfg: str):
-    """HBM bytes per launch from the committed PMC profiles (FETCH_SIZE x the gfx950
-    calibration + WRITE_SIZE, separate rocprofv3 passes); (bytes, source) or (None, None)."""
+    """HBM bytes per step from the committed PMC profile of this round's kernels
+    (FETCH_SIZE x the gfx950 calibration + WRITE_SIZE, separate rocprofv3 passes;
+    a step's bytes summed over its kernels); (bytes, source) or (None, None)."""
     try:
         with open(os.path.join(ROOT, PMC_FILE)) as f:
             return json.load(f)["configs"][f"{cfg}_auto"]["hbm_bytes"], PMC_FILE
     except (OSError, KeyError, ValueError):
-        pass
-    try:
-        with open(os.path.join(ROOT, TRAFFIC_FILE)) as f:
-            return json.load(f)["configs"][cfg]["traffic_bytes_per_launch"], TRAFFIC_FILE
-    except (OSError, KeyError, ValueError):
         return None, None
+
+
+PEAK_CLOCK_GHZ = 2.4
+
+
+def clock_reading(eng) -> dict:
+    """The clock the GPU held right after a timed region: msha_clock_probe (a
+    ~1 ms probe kernel with the hash kernels' VALU mix at 8 waves per SIMD,
+    in-kernel s_memtime / s_memrealtime; the hash kernels carry no stamps).
+    frac_at_clock (in roofline) = frac x 2.4 GHz / this clock: the share of the
+    peak at the clock the chip actually held."""
+    try:
+        c = eng.clock_probe()
+    except Exception as e:  # noqa: BLE001 -- a diagnostic, never fatal to the line
+        return {"error": repr(e)[:200]}
+    return {"effective_clock_ghz": c["ghz_median"], "min": c["ghz_min"], "max": c["ghz_max"],
+            "probe_ms": c["kernel_ms"], "probe_gblocks_per_s": c["gblocks_per_s"],
+            "method": "msha_clock_probe right after the timed steps: median over workgroups of "
+                      "d(s_memtime) / d(s_memrealtime) x 100 MHz"}
 
 
 def verify_sample(w, d_out, k: int = 512) -> None:
@@ -388,11 +407,14 @@ def hashed_blocks(w, cfg: str) -> int:
     return int(((L >> np.uint64(6)) + np.where((L & np.uint64(63)) < 56, 1, 2).astype(np.uint64)).sum())
 
 
-def roofline(w, kern_ms: float, cfg: str) -> dict:
+def roofline(w, kern_ms: float, cfg: str, clock: dict | None = None) -> dict:
     achieved = OPS_PER_BLOCK * hashed_blocks(w, cfg) / (kern_ms * 1e-3) / 1e12
     traffic, src = measured_traffic(cfg)
+    ghz = (clock or {}).get("effective_clock_ghz")
     return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS,
             "unit": "Tint32op/s", "frac": achieved / PEAK_VALU_TOPS,
+            "effective_clock_ghz": ghz,
+            "frac_at_clock": achieved / PEAK_VALU_TOPS * PEAK_CLOCK_GHZ / ghz if ghz else None,
             "traffic": traffic, "traffic_source": src, "ops_per_block": OPS_PER_BLOCK,
             "note": "peak = full-rate int32 VALU (VOP2/v_bitop3, 2 cycles per wave64 "
                     "instr at 2.4 GHz); SHA-256's mix is ~60% half-rate ops (v_alignbit, "
@@ -414,14 +436,17 @@ def extra_config(eng, cfg: str, args, dev, stream, w=None) -> dict:
     step, d_out = kernel_step(eng, w, cfg, dev, stream)
     st0 = eng.stats()
     elapsed, kern_ms, warm, warmup_ms = time_steps(step, args, dev, stream)
+    clock = clock_reading(eng)
     eng.device_status()
     kind = kind_of(st0, eng.stats())
     verify_sample(w, d_out)
-    rf = roofline(w, kern_ms, cfg)
+    rf = roofline(w, kern_ms, cfg, clock)
     out = {"workload": w.name, "value": w.n * args.steps / elapsed, "unit": "digests/s",
            "gbps_hashed": w.message_bytes * args.steps / elapsed / 1e9,
            "ms_per_step": elapsed / args.steps * 1e3, "kernel_ms_mean": kern_ms, "kernel": kind,
            "frac": rf["frac"], "achieved": rf["achieved"], "traffic": rf["traffic"],
+           "traffic_source": rf["traffic_source"], "effective_clock_ghz": rf["effective_clock_ghz"],
+           "frac_at_clock": rf["frac_at_clock"],
            "blocks": w.blocks, "hashed_blocks": hashed_blocks(w, cfg),
            "verified": "512 digests vs oracle (stride not a multiple of 64)",
            "warmup_steps_run": warm}
@@ -445,6 +470,7 @@ def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist, form: st
     step, d_out = kernel_step(eng, w, form, dev, stream)
     st0 = eng.stats()
     elapsed, kern_ms, warm, _ = time_steps(step, args, dev, stream, barrier=dist.barrier)
+    clock = clock_reading(eng)
     dist.barrier()
     eng.device_status()
     kind = kind_of(st0, eng.stats())
@@ -465,6 +491,7 @@ def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist, form: st
             "kernel_ms_mean_max_over_ranks": kern_max, "kernel": kind,
             "frac": achieved / (PEAK_VALU_TOPS * world), "achieved": achieved, "peak": PEAK_VALU_TOPS * world,
             "blocks": int(blocks), "hashed_blocks": int(hashed),
+            "effective_clock_ghz_rank0": clock.get("effective_clock_ghz"),
             "verified": "512 digests per rank vs oracle (stride not a multiple of 64)",
             "warmup_steps_run": warm}
 
@@ -565,6 +592,7 @@ def main():
     st0 = eng.stats()
     elapsed, kern_ms, warm, warmup_ms = time_steps(step, args, dev, stream,
                                                    barrier=dist.barrier if world > 1 else None)
+    clock = clock_reading(eng)
     if world > 1:
         dist.barrier()
     eng.device_status()
@@ -602,11 +630,14 @@ def main():
             "data": "synthetic (splitmix64 seed 0x4D49524246540000), inputs resident in HBM",
             "config": {"workload": w.name, "config": args.config, "messages_per_gpu": w.n,
                        "message_bytes_per_gpu": w.message_bytes, "blocks_per_gpu": w.blocks,
+                       "hashed_blocks_per_gpu": hashed_blocks(w, args.config),
                        "parallelism": f"independent shards x{world}"},
             "gbps_hashed": gbps,
             "kernel_ms_mean": kern_ms,
             "kernel": kind,
-            "roofline": roofline(w, kern_ms, args.config),
+            "effective_clock_ghz": clock.get("effective_clock_ghz"),
+            "clock": clock,
+            "roofline": roofline(w, kern_ms, args.config, clock),
         }
         if world == 1 and args.config == "c2" and not args.no_extra:
             del step, d_out

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 7u
+#define MSHA_ABI_VERSION 8u
 
 enum {
   MSHA_OK = 0,
@@ -207,7 +207,10 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
  * the launch (a mixed storm sharded over several GPUs), run on the cooperative
  * kernel beside the lane kernel (a side stream forked from and joined back to
  * `stream`). Same arena rules and error reporting as msha_digest_batch_device;
- * n < 2^32 - 1. Returns after enqueueing.
+ * n < 2^32 - 1. Returns after enqueueing. Not capturable into a HIP graph: the
+ * call orders itself after the previous planned call through a library event
+ * and forks to a library-owned stream, so on a capturing stream it fails with
+ * MSHA_ERR_INVALID_ARG (msha_digest_batch_device captures).
  */
 enum { MSHA_PLAN_FOLD_ALIASES = 1u };
 int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, const uint64_t* d_off,
@@ -239,6 +242,26 @@ int msha_device_status(msha_ctx* ctx);
  */
 enum { MSHA_KERNEL_AUTO = 0, MSHA_KERNEL_LANE = 1, MSHA_KERNEL_COOP = 2 };
 int msha_set_kernel_policy(msha_ctx* ctx, int policy);
+
+/*
+ * Diagnostics (ABI 8): the clock the context's first GPU holds under the hash
+ * kernels' instruction mix. A probe kernel compresses register-resident blocks
+ * at the lane kernel's occupancy (8 waves per SIMD) and stamps s_memtime (shader
+ * clock) and s_memrealtime (100 MHz) at each workgroup's start and end; the
+ * clock is their ratio. Synchronous; run it right after the work whose clock
+ * matters (the hash kernels carry no stamps). blocks_per_lane in [1, 100000]
+ * (48: about 1 ms).
+ */
+typedef struct {
+  double ghz_median;     /* over workgroups */
+  double ghz_min;
+  double ghz_max;
+  double kernel_ms;      /* the probe launch, HIP events */
+  double gblocks_per_s;  /* register-resident compression rate of the probe */
+  uint32_t workgroups;
+  uint32_t blocks_per_lane;
+} msha_clock_info;
+int msha_clock_probe(msha_ctx* ctx, uint32_t blocks_per_lane, msha_clock_info* out);
 
 /* Pinned host memory for callers that want zero-copy staging: when the arena
  * passed to msha_digest_batch lies in such memory, every message start is

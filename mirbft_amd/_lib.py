@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -79,6 +79,18 @@ class MshaShardStats(ctypes.Structure):
     ]
 
 
+class MshaClockInfo(ctypes.Structure):
+    _fields_ = [
+        ("ghz_median", ctypes.c_double),
+        ("ghz_min", ctypes.c_double),
+        ("ghz_max", ctypes.c_double),
+        ("kernel_ms", ctypes.c_double),
+        ("gblocks_per_s", ctypes.c_double),
+        ("workgroups", ctypes.c_uint32),
+        ("blocks_per_lane", ctypes.c_uint32),
+    ]
+
+
 # name -> (restype, argtypes)
 SIGNATURES = {
     "msha_abi_version": (ctypes.c_uint32, []),
@@ -110,6 +122,7 @@ SIGNATURES = {
                                                      ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
                                                      ctypes.c_void_p]),
     "msha_device_status": (ctypes.c_int, [_ctxp]),
+    "msha_clock_probe": (ctypes.c_int, [_ctxp, ctypes.c_uint32, ctypes.POINTER(MshaClockInfo)]),
     "msha_set_kernel_policy": (ctypes.c_int, [_ctxp, ctypes.c_int]),
     "msha_pinned_alloc": (ctypes.c_int, [_ctxp, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]),
     "msha_pinned_free": (ctypes.c_int, [_ctxp, ctypes.c_void_p]),

@@ -874,6 +874,12 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
 // producer wave (64 messages: loads, padding, K+W schedules into LDS, as in
 // k_digest_coop) and two consumer waves of 32 messages; EXCL as above (the
 // head's CUs hold nothing else); each lane stores its side's four digest words.
+// Both DPP adds sit in ONE asm statement with an s_nop 0 between them: a DPP
+// read of a VGPR needs 2 wait states after the VALU write of it, the compiler's
+// hazard recognizer does not look inside asm text, and u_ (read through DPP by
+// the second add) may be written by the instruction right before the first.
+// The first add's DPP source (W) was written four rounds earlier.
+// tools/check_dpp_hazards.py checks every DPP of the built library for it.
 // ---------------------------------------------------------------------------
 #define MSHA_DROUND(X, Y, Z, W, kw)                                                              \
   {                                                                                              \
@@ -881,10 +887,10 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
                              __builtin_amdgcn_alignbit(X, X, sh3));                              \
     const uint32_t u_ = s_ + ch(X, Y, Z) + (W + (kw));                                           \
     uint32_t t_ = s_ + maj(X, Y, Z) + (kw);                                                      \
-    asm volatile("v_add_u32_dpp %0, %1, %2 row_mirror row_mask:0xf bank_mask:0x3"                \
+    asm volatile("v_add_u32_dpp %0, %1, %2 row_mirror row_mask:0xf bank_mask:0x3\n\t"            \
+                 "s_nop 0\n\t"                                                                   \
+                 "v_add_u32_dpp %0, %2, %0 row_mirror row_mask:0xf bank_mask:0xc"                \
                  : "+v"(t_) : "v"(W), "v"(u_));                                                  \
-    asm volatile("v_add_u32_dpp %0, %1, %0 row_mirror row_mask:0xf bank_mask:0xc"                \
-                 : "+v"(t_) : "v"(u_));                                                          \
     W = t_;                                                                                      \
   }
 #define MSHA_D4(q)                                 \
@@ -1030,6 +1036,47 @@ __global__ __launch_bounds__(256, DigestSrc::kMinWaves) void k_digest_of_digests
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   DigestSrc{table, idx, begin}.full<0>(i, out);
+}
+
+// ---------------------------------------------------------------------------
+// Clock probe (msha_clock_probe; bench.py's effective_clock_ghz). The compression
+// on register-resident data at the lane kernel's occupancy (8 waves per SIMD,
+// the same VALU mix), with one (s_memtime, s_memrealtime) pair stamped by the
+// first lane of each workgroup at its start and end: the in-kernel clock is
+// d(memtime) / d(memrealtime) x 100 MHz (MI355X_MICROARCH.md, DVFS item 6).
+// A separate kernel: the hash kernels carry no stamps. Run right after a timed
+// region, it reads the clock the chip holds under this instruction mix.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 8) void k_clock_probe(uint32_t blocks, uint64_t* __restrict__ stamps,
+                                                        uint32_t* __restrict__ sink) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+  State s;
+  state_init(s);
+  uint32_t w[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) w[k] = (blockIdx.x * 256 + threadIdx.x) * 16 + k;
+  for (uint32_t b = 0; b < blocks; ++b) {
+    compress(s, w);
+    w[0] ^= s.h[0];  // the next block depends on this one
+  }
+  const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x == 0) {
+    uint64_t* st = stamps + 4 * (uint64_t)blockIdx.x;
+    st[0] = t0;
+    st[1] = r0;
+    st[2] = t1;
+    st[3] = r1;
+  }
+  uint32_t x = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) x ^= s.h[k];
+  if (x == 0x9E3779B9u) sink[0] = x;  // keeps the work; practically never stores
+}
+
+hipError_t launch_clock_probe(uint32_t blocks, uint32_t workgroups, uint64_t* stamps, uint32_t* sink,
+                              hipStream_t st) {
+  hipLaunchKernelGGL(k_clock_probe, dim3(workgroups), dim3(256), 0, st, blocks, stamps, sink);
+  return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------

@@ -108,7 +108,8 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t st);
 // kNoLane past the last; info[1] = the head of lanes whose chains would outlast
 // the lane kernel's throughput time, for the cooperative kernel (at most
 // head_cap). Block-count buckets: exact below 4,096 blocks, powers of two above.
-constexpr uint32_t kFoldBuckets = 4096 + 52;
+constexpr uint32_t kFoldBigBuckets = 52;  // the power-of-two classes (>= 4,096 blocks): keys [0, 52)
+constexpr uint32_t kFoldBuckets = 4096 + kFoldBigBuckets;
 struct FoldArgs {
   const uint64_t* off;
   const uint64_t* len;
@@ -118,6 +119,9 @@ struct FoldArgs {
   uint32_t* rep = nullptr;    // n (with table): the lane message i's digest comes from
   uint64_t* tmax = nullptr;   // (with table) ceil(n / 4096): largest offset before each tile
   uint32_t* cnt;              // kFoldBuckets zeroed counters -> bucket starts
+  uint64_t* big = nullptr;    // 2 x kFoldBigBuckets zeroed: per power-of-two key, the largest
+                              // block count and the block sum (the head's cost model needs the
+                              // real longest chain, not the class's lower bound)
   uint32_t* order;            // n, kNoLane-filled -> position -> message index
   uint32_t* info;             // out: [0] lanes, [1] head
   uint32_t head_cap = 0;      // 0: no head
@@ -141,5 +145,11 @@ struct FoldArgs {
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st);
 // out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.
 hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st);
+
+// Clock probe (msha_clock_probe): `workgroups` x 256 lanes compress `blocks`
+// register-resident blocks each; stamps gets (memtime, memrealtime) at start and
+// end per workgroup, 4 words each.
+hipError_t launch_clock_probe(uint32_t blocks, uint32_t workgroups, uint64_t* stamps, uint32_t* sink,
+                              hipStream_t st);
 
 }  // namespace msha

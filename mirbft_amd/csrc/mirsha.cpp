@@ -238,6 +238,7 @@ struct Device {
   // representatives, bucket counters, lane order, [lanes | head]; the head of
   // long chains runs on side_stream, forked from and joined to the caller's
   DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_info;
+  DevBuf probe;  // msha_clock_probe: stamps + sink
   hipStream_t side_stream = nullptr;
   hipEvent_t ev_fork = nullptr, ev_fplan = nullptr, ev_join = nullptr, ev_fdone = nullptr;
   bool fdone_recorded = false;  // ev_fdone: the last planned call's work is queued behind it
@@ -259,7 +260,7 @@ struct Device {
     gather_pool.reset();
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table, &sm_in, &sm_out, &p_meta,
                       &p_gmap, &p_devoff, &p_table, &p_slot, &p_rep, &p_cnt, &p_small, &f_table, &f_rep,
-                      &f_tmax, &f_cnt, &f_order, &f_info})
+                      &f_tmax, &f_cnt, &f_order, &f_info, &probe})
       b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
@@ -2506,6 +2507,15 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     hipStream_t st;
     device_prologue(ctx, stream, &st);
     Device& d = ctx->devs[0];
+    // Not capturable into a HIP graph (mirsha.h): the call waits on the previous
+    // planned call's event, recorded outside any capture, and forks to and joins
+    // from a library-owned side stream. Say so instead of failing inside HIP.
+    hipStreamCaptureStatus cap_status = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(st, &cap_status));
+    if (cap_status != hipStreamCaptureStatusNone)
+      throw MshaError(MSHA_ERR_INVALID_ARG,
+                     "msha_digest_batch_device_planned cannot be captured into a HIP graph; "
+                     "use msha_digest_batch_device there");
     const bool fold = flags & MSHA_PLAN_FOLD_ALIASES;
     // Few messages: one cooperative launch over the planned order (every
     // workgroup gets a CU); otherwise the lane kernel, its longest chains
@@ -2514,7 +2524,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     const bool head = !all_coop && ctx->kernel_policy != MSHA_KERNEL_LANE && env_u64("MSHA_PLAN_HEAD", 1) != 0;
     uint64_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
-    d.f_cnt.ensure(4 * msha::kFoldBuckets);
+    d.f_cnt.ensure(4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets);  // counters, then FoldArgs::big
     d.f_order.ensure(4 * n);
     d.f_info.ensure(8);
     if (fold) {
@@ -2543,7 +2553,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       ps = d.side_stream;
     }
     if (fold) HIPCHK(hipMemsetAsync(d.f_table.p, 0, 4 * cap, ps));
-    HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, 4 * msha::kFoldBuckets, ps));
+    HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets, ps));
     HIPCHK(hipMemsetAsync(d.f_order.p, 0xFF, 4 * n, ps));  // kNoLane
     msha::FoldArgs fa;
     fa.off = d_off;
@@ -2554,6 +2564,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.rep = fold ? d.f_rep.as<uint32_t>() : nullptr;
     fa.tmax = fold ? d.f_tmax.as<uint64_t>() : nullptr;
     fa.cnt = d.f_cnt.as<uint32_t>();
+    fa.big = reinterpret_cast<uint64_t*>(fa.cnt + msha::kFoldBuckets);  // 4 x 4,148 B: 8-byte aligned
     fa.order = d.f_order.as<uint32_t>();
     fa.info = d.f_info.as<uint32_t>();
     fa.simds = (uint32_t)d.cus * 4;
@@ -2679,6 +2690,54 @@ int msha_device_status(msha_ctx* ctx) {
   if (flag & 2) return fail(ctx, MSHA_ERR_HIP, "split-chain handoff timed out (digests undefined)");
   if (flag) return fail(ctx, MSHA_ERR_ALIGNMENT, "device arena message start not 16-byte aligned");
   return MSHA_OK;
+}
+
+int msha_clock_probe(msha_ctx* ctx, uint32_t blocks_per_lane, msha_clock_info* out) {
+  if (!ctx || ctx->devs.empty() || !out || blocks_per_lane == 0 || blocks_per_lane > 100000)
+    return MSHA_ERR_INVALID_ARG;
+  std::lock_guard<std::mutex> lock(ctx->mu);
+
+  return guarded(ctx, [&] {
+    Device& d = ctx->devs[0];
+    HIPCHK(hipSetDevice(d.id));
+    const uint32_t wgs = (uint32_t)d.cus * 8;  // 8 waves per SIMD, as the lane kernel runs
+    d.probe.ensure(32ull * wgs + 64);
+    uint64_t* stamps = d.probe.as<uint64_t>();
+    uint32_t* sink = reinterpret_cast<uint32_t*>(stamps + 4ull * wgs);
+    hipEvent_t e0, e1;
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    struct Ev {
+      hipEvent_t a, b;
+      ~Ev() {
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+      }
+    } ev{e0, e1};
+    HIPCHK(hipEventRecord(e0, d.stream));
+    HIPCHK(msha::launch_clock_probe(blocks_per_lane, wgs, stamps, sink, d.stream));
+    HIPCHK(hipEventRecord(e1, d.stream));
+    HIPCHK(hipStreamSynchronize(d.stream));
+    float ms = 0;
+    HIPCHK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<uint64_t> h(4ull * wgs);
+    HIPCHK(hipMemcpy(h.data(), stamps, 8 * h.size(), hipMemcpyDeviceToHost));
+    std::vector<double> ghz;
+    ghz.reserve(wgs);
+    for (uint32_t g = 0; g < wgs; ++g) {
+      const uint64_t dt = h[4 * g + 2] - h[4 * g], dr = h[4 * g + 3] - h[4 * g + 1];
+      if (dr > 0) ghz.push_back((double)dt / (double)dr * 0.1);  // memrealtime: 100 MHz
+    }
+    if (ghz.empty()) throw MshaError(MSHA_ERR_HIP, "clock probe: no workgroup advanced memrealtime");
+    std::sort(ghz.begin(), ghz.end());
+    out->ghz_median = ghz[ghz.size() / 2];
+    out->ghz_min = ghz.front();
+    out->ghz_max = ghz.back();
+    out->kernel_ms = ms;
+    out->workgroups = wgs;
+    out->blocks_per_lane = blocks_per_lane;
+    out->gblocks_per_s = ms > 0 ? (double)wgs * 256 * blocks_per_lane / (ms * 1e-3) / 1e9 : 0;
+  });
 }
 
 int msha_pinned_alloc(msha_ctx* ctx, uint64_t bytes, void** p) {

@@ -418,17 +418,40 @@ static_assert(kFoldTile <= 4096 && (kFoldBuckets << 12) < kEmptyKey, "scatter pa
 
 __global__ __launch_bounds__(256) void k_fold_keys(FoldArgs a) {
   __shared__ uint32_t hist[kFoldBuckets];
+  __shared__ unsigned long long bmax[kFoldBigBuckets], bsum[kFoldBigBuckets];
   for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x) hist[j] = 0;
+  if (threadIdx.x < kFoldBigBuckets) bmax[threadIdx.x] = bsum[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
 #pragma unroll 4
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    if (i < a.n && (!a.table || a.rep[i] == (uint32_t)i)) atomicAdd(&hist[fold_key(a.len[i])], 1u);
+    if (i < a.n && (!a.table || a.rep[i] == (uint32_t)i)) {
+      const uint64_t blocks = dev_blocks_for(a.len[i]);
+      const uint32_t k = kFoldBuckets - 1 - fold_bucket(blocks);
+      atomicAdd(&hist[k], 1u);
+      if (k < kFoldBigBuckets) {  // >= 4,096 blocks (1/4 MiB): rare
+        atomicMax(&bmax[k], (unsigned long long)blocks);
+        atomicAdd(&bsum[k], (unsigned long long)blocks);
+      }
+    }
   }
   __syncthreads();
   for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
     if (hist[j]) atomicAdd(&a.cnt[j], hist[j]);
+  if (threadIdx.x < kFoldBigBuckets && bsum[threadIdx.x]) {
+    atomicMax(reinterpret_cast<unsigned long long*>(&a.big[threadIdx.x]), bmax[threadIdx.x]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.big[kFoldBigBuckets + threadIdx.x]), bsum[threadIdx.x]);
+  }
+}
+
+// Key k's longest chain and its c lanes' blocks: exact below 4,096 blocks (one
+// class per count), measured by k_fold_keys for the power-of-two classes above.
+__device__ __forceinline__ uint64_t key_max_blocks(const FoldArgs& a, uint32_t k) {
+  return k < kFoldBigBuckets ? a.big[k] : fold_bucket_blocks(kFoldBuckets - 1 - k);
+}
+__device__ __forceinline__ uint64_t key_sum_blocks(const FoldArgs& a, uint32_t k, uint32_t c) {
+  return k < kFoldBigBuckets ? a.big[kFoldBigBuckets + k] : (uint64_t)c * fold_bucket_blocks(kFoldBuckets - 1 - k);
 }
 
 // The head. Per candidate cut k (lanes with keys below k -- the longest -- go
@@ -462,7 +485,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   for (uint32_t b = b0; b < b1; ++b) {
     const uint32_t c = a.cnt[b];
     s += c;
-    bl += (uint64_t)c * fold_bucket_blocks(kFoldBuckets - 1 - b);
+    bl += key_sum_blocks(a, b, c);
   }
   part[t] = s;
   blk[t] = bl;
@@ -490,7 +513,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     __syncthreads();
   }
   const uint32_t kmax = (uint32_t)best[0];
-  const uint64_t max_blocks = kmax < kFoldBuckets ? fold_bucket_blocks(kFoldBuckets - 1 - kmax) : 0;
+  const uint64_t max_blocks = kmax < kFoldBuckets ? key_max_blocks(a, kmax) : 0;
   __syncthreads();
   // each thread: the best cut at its buckets' boundaries, packed (cost, key)
   uint32_t run = part[t] - s;
@@ -500,7 +523,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   for (uint32_t b = b0; b < b1; ++b) {  // cut before bucket b: h = run, its longest = bucket b
     const uint32_t c = a.cnt[b];
     if (c && a.head_cap) {
-      const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, fold_bucket_blocks(kFoldBuckets - 1 - b));
+      const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, key_max_blocks(a, b));
       const uint64_t key = (min(cost, kCostMax) << 20) | b;
       if (key < mine) {
         mine = key;
@@ -509,7 +532,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     }
     a.cnt[b] = run;
     run += c;
-    brun += (uint64_t)c * fold_bucket_blocks(kFoldBuckets - 1 - b);
+    brun += key_sum_blocks(a, b, c);
   }
   if (t == 1023 && a.head_cap) {  // the cut after the last bucket: every lane on the head
     const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, 0);

@@ -215,7 +215,43 @@ class Engine:
             return None
         return int(getattr(stream, "cuda_stream", stream))
 
+    def _device_index(self) -> int:
+        n = ctypes.c_uint32(0)
+        self._check(self._lib.msha_shard_count(self._ctx, ctypes.byref(n)))
+        s = L.MshaShardStats()
+        self._check(self._lib.msha_get_shard_stats(self._ctx, 0, ctypes.byref(s)))
+        return int(s.device)
+
+    def _check_device_args(self, n: int, out, **tensors) -> None:
+        """The *_device entry points take raw device pointers: check here what
+        the C ABI cannot -- every tensor contiguous on the context's first GPU,
+        8-byte integers for off/len/begin, 4-byte for order/idx, out a uint8
+        buffer of at least 32 n bytes -- so a mismatch raises instead of
+        reading or writing out of bounds on the GPU."""
+        import torch
+        dev = getattr(self, "_dev_index", None)
+        if dev is None:
+            dev = self._dev_index = self._device_index()
+        sizes = {"off": 8, "length": 8, "begin": 8, "order": 4, "idx": 4, "arena": 1, "table": 1}
+        for name, t in list(tensors.items()) + [("out", out)]:
+            if t is None:
+                continue
+            if not isinstance(t, torch.Tensor) or t.device.type != "cuda" or t.device.index != dev:
+                raise ValueError(f"{name} must be a torch tensor on cuda:{dev} (the context's first GPU)")
+            if not t.is_contiguous():
+                raise ValueError(f"{name} must be contiguous")
+            want = 1 if name == "out" else sizes[name]
+            if t.element_size() != want or t.is_floating_point():
+                raise ValueError(f"{name} must hold {want}-byte integers (got {t.dtype})")
+        for name in ("off", "length", "order"):
+            t = tensors.get(name)
+            if t is not None and t.numel() != n:
+                raise ValueError(f"{name} has {t.numel()} entries, expected {n}")
+        if out.numel() < 32 * n:
+            raise ValueError(f"out holds {out.numel()} bytes, needs {32 * n}")
+
     def digest_batch_device(self, arena, off, length, out, stream=None, order=None) -> None:
+        self._check_device_args(off.numel(), out, arena=arena, off=off, length=length, order=order)
         self._check(self._lib.msha_digest_batch_device(self._ctx, arena.data_ptr(), off.data_ptr(),
                                                        length.data_ptr(),
                                                        None if order is None else order.data_ptr(),
@@ -224,19 +260,29 @@ class Engine:
     def digest_batch_device_planned(self, arena, off, length, out, stream=None, fold: bool = False) -> None:
         """msha_digest_batch_device_planned: lane order (and, with fold, alias
         folding) planned on the GPU inside the call's launches."""
+        self._check_device_args(off.numel(), out, arena=arena, off=off, length=length)
         self._check(self._lib.msha_digest_batch_device_planned(self._ctx, arena.data_ptr(), off.data_ptr(),
                                                                length.data_ptr(), off.numel(),
                                                                1 if fold else 0, out.data_ptr(),
                                                                self._stream_ptr(stream)))
 
     def digest_uniform_device(self, arena, stride: int, msg_len: int, n: int, out, stream=None) -> None:
+        self._check_device_args(n, out, arena=arena)
         self._check(self._lib.msha_digest_uniform_device(self._ctx, arena.data_ptr(), stride, msg_len, n,
                                                          out.data_ptr(), self._stream_ptr(stream)))
 
     def digest_of_digests_device(self, table, idx, begin, out, stream=None) -> None:
+        self._check_device_args(begin.numel() - 1, out, table=table, idx=idx, begin=begin)
         self._check(self._lib.msha_digest_of_digests_device(self._ctx, table.data_ptr(), idx.data_ptr(),
                                                             begin.data_ptr(), begin.numel() - 1,
                                                             out.data_ptr(), self._stream_ptr(stream)))
+
+    def clock_probe(self, blocks_per_lane: int = 48) -> dict:
+        """msha_clock_probe: the clock the first GPU holds under the hash
+        kernels' instruction mix (in-kernel s_memtime / s_memrealtime)."""
+        c = L.MshaClockInfo()
+        self._check(self._lib.msha_clock_probe(self._ctx, int(blocks_per_lane), ctypes.byref(c)))
+        return {name: getattr(c, name) for name, _ in L.MshaClockInfo._fields_}
 
     def device_status(self) -> None:
         self._check(self._lib.msha_device_status(self._ctx))

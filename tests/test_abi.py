@@ -29,7 +29,7 @@ def test_exports_via_nm():
 
 
 def test_abi_version():
-    assert L.lib().msha_abi_version() == L.ABI_VERSION == 7
+    assert L.lib().msha_abi_version() == L.ABI_VERSION == 8
 
 
 def test_library_is_gfx950_code_object():
@@ -213,3 +213,64 @@ def test_alias_first_matches_dict(case):
     got = alias_first(off, ln)
     exp = _first_ref(off, ln)
     assert np.array_equal(got, exp)
+
+
+def _dpp_checker():
+    import importlib.util
+    import os
+    p = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "check_dpp_hazards.py")
+    spec = importlib.util.spec_from_file_location("check_dpp_hazards", p)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_dpp_hazard_checker_flags_a_close_write():
+    """The checker itself: a VALU write of the DPP source one instruction before
+    is a hazard, two instructions or an s_nop 0 + one instruction before is not."""
+    m = _dpp_checker()
+    body = ["f:", "v_add3_u32 v90, v79, v59, v91", "v_bitop3_b32 v91, v78, v61, v60 bitop3:0xe8",
+            "v_add_u32_e32 v79, v79, v91"]
+    ok = body + ["v_add_u32_dpp v79, v59, v90 row_mirror row_mask:0xf bank_mask:0x3", "s_nop 0",
+                 "v_add_u32_dpp v79, v90, v79 row_mirror row_mask:0xf bank_mask:0xc"]
+    assert m.check(ok) == (2, [])
+    bad = ["f:", "v_add3_u32 v90, v79, v59, v91", "v_add_u32_e32 v79, v79, v91",
+           "v_add_u32_dpp v79, v90, v79 row_mirror row_mask:0xf bank_mask:0xc"]
+    n, hz = m.check(bad)
+    assert n == 1 and len(hz) == 1 and "1 wait state" in hz[0]
+    assert len(m.check(["f:", "v_add_u32_dpp v1, v2, v3 row_mirror"])[1]) == 1   # block start: unknown
+
+
+def test_no_dpp_read_hazard_in_device_code():
+    """k_digest_chain2's DPP adds are inline asm (the compiler's hazard recognizer
+    does not see them): every DPP of the built library has its 2 wait states."""
+    import os
+    m = _dpp_checker()
+    if not os.path.exists(f"{m.LLVM}/llvm-objdump"):
+        pytest.skip("no ROCm llvm-objdump")
+    n, hz = m.check(m.disassemble(L.LIB_PATH))
+    assert n >= 128 and hz == [], hz[:5]
+
+
+def test_device_entry_points_validate_tensors_before_the_call():
+    """engine.*_device take raw device pointers: wrong device, dtype width,
+    contiguity or a short out must raise before anything reaches the C ABI."""
+    import torch
+    from mirbft_amd.engine import Engine
+    eng = Engine.__new__(Engine)      # no context needed: validation runs first
+    eng._dev_index = 0
+    eng._ctx = None
+
+    class NoCall:
+        def __getattr__(self, name):
+            raise AssertionError(f"{name} called")
+    eng._lib = NoCall()
+    arena = torch.zeros(128, dtype=torch.uint8)
+    off = torch.zeros(2, dtype=torch.int64)
+    out = torch.zeros((2, 32), dtype=torch.uint8)
+    with pytest.raises(ValueError, match="cuda:0"):
+        eng.digest_batch_device(arena, off, off, out)
+    with pytest.raises(ValueError, match="cuda:0"):
+        eng.digest_batch_device_planned(arena, off, off, out)
+    with pytest.raises(ValueError, match="cuda:0"):
+        eng.digest_of_digests_device(arena.view(-1, 32), off.int(), off, out)

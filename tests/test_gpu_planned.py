@@ -231,3 +231,52 @@ def test_bad_flags(engine):
     rc = L.lib().msha_digest_batch_device_planned(engine._ctx, t.data_ptr(), o.data_ptr(), o.data_ptr(), 1,
                                                   2, t.data_ptr(), None)
     assert rc == L.MSHA_ERR_INVALID_ARG
+
+
+def test_big_bucket_messages_head(engine, monkeypatch):
+    """Messages of 4,096 blocks or more share power-of-two block-count classes;
+    the planner's head cost model reads each class's real longest chain and
+    block sum (k_fold_keys). A batch whose longest chains sit in those classes
+    (5,000 - 9,000 blocks, one class) among many small requests: every digest
+    exact, folded and not, with the head on either kernel."""
+    rng = np.random.default_rng(4096)
+    n = 40_000
+    ln = np.full(n, 512, np.uint64)
+    longs = rng.choice(n, 24, replace=False)
+    ln[longs] = rng.integers(5000 * 64, 9000 * 64, longs.size).astype(np.uint64)
+    off = np.concatenate([[0], np.cumsum((ln + np.uint64(15)) // np.uint64(16) * np.uint64(16))[:-1]]).astype(np.uint64)
+    arena = W.random_bytes(W.SEED ^ 0x4096, 0, int(off[-1] + ln[-1]) + 64)
+    w = W.Workload("big-bucket", arena, off, ln)
+    exp = _expect(w)
+    for chain2 in ("0", "2"):
+        monkeypatch.setenv("MSHA_HEAD_CHAIN2", chain2)
+        for fold in (False, True):
+            before = engine.stats()
+            assert np.array_equal(_run(engine, w, fold), exp)
+            assert _delta(before, engine.stats(), "launches_coop") == 1   # the long chains got a head
+
+
+def test_graph_capture_refused_cleanly(engine):
+    """The planned call cannot be captured into a HIP graph (mirsha.h): on a
+    capturing stream it fails with MSHA_ERR_INVALID_ARG and names the reason,
+    and the context keeps working afterwards."""
+    import torch
+    from mirbft_amd import _lib as L
+    w = W.c5_storm(n=1 << 12, first=3)
+    d_arena, d_off, d_len = _dev(w)
+    out = torch.zeros((w.n, 32), dtype=torch.uint8, device="cuda:0")
+    assert np.array_equal(_run(engine, w, True), _expect(w))   # scratch allocated outside the capture
+    s = torch.cuda.Stream()
+    g = torch.cuda.CUDAGraph()
+    err = None
+    with torch.cuda.stream(s):
+        g.capture_begin()
+        try:
+            engine.digest_batch_device_planned(d_arena, d_off, d_len, out, stream=s, fold=True)
+        except MshaError as e:
+            err = e
+        finally:
+            g.capture_end()
+    assert err is not None and err.code == L.MSHA_ERR_INVALID_ARG and "graph" in str(err)
+    torch.cuda.synchronize()
+    assert np.array_equal(_run(engine, w, True), _expect(w))

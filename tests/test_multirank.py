@@ -103,5 +103,8 @@ def test_bench_two_ranks_on_the_engine():
     assert d["extra_configs"]["c5_folded"]["hashed_blocks"] < c5["blocks"] == d["extra_configs"]["c5_planned"]["hashed_blocks"]
     # the CPU baseline at N > 1 too (rank 0, after the ranks released their GPUs)
     cb = d["cpu_baseline"]
-    assert cb["kind"] == "port" and cb["cores"] == 1 and cb["value"] > 0 and cb["impl"]
+    # value = OpenSSL SHA-NI on one thread (the kind says so); the scalar port beside it
+    assert cb["kind"] == "openssl-sha-ni-1-thread (proxy for Go crypto/sha256)"
+    assert cb["cores"] == 1 and cb["value"] == cb["openssl"]["1_thread"]["value"] and cb["impl"]
+    assert cb["scalar_port"]["value"] > 0
     assert d["host_api"]["first_launch_ms_max"] > 0

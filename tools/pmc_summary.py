@@ -3,13 +3,23 @@
 config) into profiles/<round>_pmc.json: the counters that justify the kernel
 choices -- VALU issue (instructions per block, SIMD cycles per instruction,
 VALUBusy, VALUUtilization), integer-op throughput against the int32 VALU peak,
-clock under load, and HBM bytes/GB/s (FETCH_SIZE x the gfx950 calibration of
-profiles/r01_traffic.json + WRITE_SIZE).
+clock under load, and HBM bytes/GB/s (FETCH_SIZE x the gfx950 calibration +
+WRITE_SIZE).
 
-    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc.json
+    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r04_pmc.json [calib.json]
 
-Only the last 3 dispatches of each run (bench.py's timed steps) are used; the
-earlier ones are warmup (the bench warms up for >= 300 ms so clocks settle).
+A bench step may run several kernels (the GPU-planned c5 forms: the k_fold_*
+planner, the head on k_digest_chain2 / k_digest_coop, the lane kernel, the alias
+fill). Every kernel whose name starts with msha:: is summarised on its own from
+its last 3 dispatches (bench.py --steps 3: the timed steps; everything before is
+warmup, >= 300 ms so clocks settle), and the step's HBM bytes are the sum over
+its kernels. Under --pmc rocprofv3 serialises dispatches, so the head and the
+lane kernel, concurrent in the bench, run one after the other here: per-kernel
+figures are exact, the step's kernel time is the serial sum.
+
+Top-level fields of a config describe its dominant hash kernel (the longest
+k_digest_*), as in earlier rounds' files, plus "kernels" (each kernel) and
+"step" (whole-step sums).
 """
 import csv
 import json
@@ -18,41 +28,72 @@ import sys
 from collections import defaultdict
 
 SRC = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
-DST = sys.argv[2] if len(sys.argv) > 2 else "profiles/r01_pmc.json"
+DST = sys.argv[2] if len(sys.argv) > 2 else "profiles/r04_pmc.json"
+CALIB = sys.argv[3] if len(sys.argv) > 3 else None
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OPS_PER_BLOCK = 1400
 PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 SIMDS, CUS, XCDS = 1024, 256, 8
 HBM_PEAK_GBS = 8000.0
+TIMED = 3  # bench.py --steps 3 in tools/pmc_valu.sh
+# waves per workgroup of the kernels that hold a CU each (heads): the CUs they occupy
+WAVES_PER_WG = {"k_digest_chain2": 3, "k_digest_coop": 4}
 
 
 def calib_factor():
+    """FETCH_SIZE -> bytes on gfx950: this run's calibration pass (calib_fetch:
+    tools/traffic_calib reads 2^29 bytes with the engine's per-lane pattern; its
+    first dispatch is cold and skipped) if present, else a given JSON, else
+    round 1's (profiles/r01_traffic.json)."""
+    f = os.path.join(SRC, "calib_fetch", "run_counter_collection.csv")
+    if os.path.exists(f):
+        per = defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if "k_read_like_c2" in r["Kernel_Name"] and r["Counter_Name"] == "FETCH_SIZE":
+                per[int(r["Dispatch_Id"])] += float(r["Counter_Value"])
+        kb = [per[d] for d in sorted(per)][1:]
+        if kb:
+            return (1 << 29) / (1024.0 * sum(kb) / len(kb)), "this run's calib_fetch pass (tools/traffic_calib)"
+    if CALIB and os.path.exists(CALIB):
+        with open(CALIB) as f:
+            return json.load(f)["calib_factor"], CALIB
     with open(os.path.join(ROOT, "profiles", "r01_traffic.json")) as f:
-        return json.load(f)["calib"]["calib_factor"]
+        return json.load(f)["calib"]["calib_factor"], "profiles/r01_traffic.json"
+
+
+def short(name):
+    return name.split("(")[0].replace("void ", "")
 
 
 def counters(run):
-    """{dispatch: {counter: value}} and {dispatch: duration_ns} for our kernels."""
-    vals = defaultdict(lambda: defaultdict(float))
+    """{kernel: [(counters, ns) for its last TIMED dispatches]} for msha:: kernels."""
     f = os.path.join(SRC, run, "run_counter_collection.csv")
     if not os.path.exists(f):
-        return None, None
+        return None
+    vals = defaultdict(lambda: defaultdict(float))
+    kname = {}
     for r in csv.DictReader(open(f)):
-        if "msha::k_digest" in r["Kernel_Name"]:
-            vals[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])
+        if "msha::k_" in r["Kernel_Name"]:
+            d = int(r["Dispatch_Id"])
+            vals[d][r["Counter_Name"]] += float(r["Counter_Value"])
+            kname[d] = short(r["Kernel_Name"])
     dur = {}
     for r in csv.DictReader(open(os.path.join(SRC, run, "run_kernel_trace.csv"))):
-        if "msha::k_digest" in r["Kernel_Name"]:
-            dur[int(r["Dispatch_Id"])] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
-    return vals, dur
+        d = int(r["Dispatch_Id"])
+        if d in kname:
+            dur[d] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+    by = defaultdict(list)
+    for d in sorted(kname):
+        by[kname[d]].append((vals[d], dur.get(d, 0)))
+    return {k: v[-TIMED:] for k, v in by.items()}
 
 
-TIMED = 3  # bench.py --steps 3 in tools/pmc_valu.sh: the last 3 dispatches are the timed ones
+def mean(rows, name):
+    return sum(c.get(name, 0.0) for c, _ in rows) / len(rows)
 
 
-def mean_timed(vals, dur, name):
-    ds = sorted(vals)[-TIMED:]   # everything before them is warmup (clocks settling)
-    return sum(vals[d].get(name, 0.0) for d in ds) / len(ds), sum(dur[d] for d in ds) / len(ds)
+def mean_ns(rows):
+    return sum(ns for _, ns in rows) / len(rows)
 
 
 def bench_line(run):
@@ -61,79 +102,106 @@ def bench_line(run):
     return json.loads(lines[-1])
 
 
-def kernel_name(run):
-    for r in csv.DictReader(open(os.path.join(SRC, run, "run_kernel_trace.csv"))):
-        if "msha::k_digest" in r["Kernel_Name"]:
-            return r["Kernel_Name"].split("(")[0].replace("void ", "")
-    return None
+def kernel_entry(k, sq, sq2, fe, wr, cf):
+    rows = sq[k]
+    ns = mean_ns(rows)
+    grbm = mean(rows, "GRBM_GUI_ACTIVE")
+    cyc = grbm / XCDS
+    insts = mean(rows, "SQ_INSTS_VALU")
+    active = mean(rows, "SQ_ACTIVE_INST_VALU")
+    waves = mean(rows, "SQ_WAVES")
+    wave_cyc = mean(rows, "SQ_WAVE_CYCLES")
+    e = {"us": ns / 1e3, "clock_ghz": cyc / ns if ns else None,
+         "valu_lane_instr": insts * 64, "salu_instr": mean(rows, "SQ_INSTS_SALU"), "waves": waves,
+         "simd_cycles_per_valu_instr": cyc * SIMDS / insts if insts else None,
+         "valu_busy_pct": 100 * active / CUS / cyc if cyc else None,
+         "wait_any_share": mean(rows, "SQ_WAIT_ANY") / wave_cyc if wave_cyc else None}
+    base = k.split("<")[0].split("::")[-1]
+    if base in WAVES_PER_WG and waves:
+        # a head: one workgroup per CU, so its figures over the CUs it holds
+        own = waves / WAVES_PER_WG[base]
+        e["occupied_cus"] = own
+        e["valu_busy_pct_own_cus"] = 100 * active / own / cyc if cyc else None
+        e["simd_cycles_per_valu_instr_own_simds"] = cyc * own * 4 / insts if insts else None
+    if sq2 and k in sq2:
+        r2 = sq2[k]
+        thr, act2 = mean(r2, "SQ_THREAD_CYCLES_VALU"), mean(r2, "SQ_ACTIVE_INST_VALU")
+        e.update({"int32_share": mean(r2, "SQ_INSTS_VALU_INT32") / insts if insts else None,
+                  "valu_utilization_pct": 100 * thr / (act2 * 64) if act2 else None,
+                  "lds_instr": mean(r2, "SQ_INSTS_LDS") * 64})
+    if fe and wr and k in fe and k in wr:
+        e["hbm_bytes"] = mean(fe[k], "FETCH_SIZE") * 1024 * cf + mean(wr[k], "WRITE_SIZE") * 1024
+        e["hbm_gbs"] = e["hbm_bytes"] / ns if ns else None
+    return e
 
 
 def main():
-    cf = calib_factor()
+    cf, cf_src = calib_factor()
     names = sorted({d.rsplit("_", 1)[0] for d in os.listdir(SRC)
                     if os.path.isdir(os.path.join(SRC, d)) and d.endswith("_sq")})
     out = {"source": "tools/pmc_valu.sh (rocprofv3 --kernel-trace --pmc, one pass per counter group); "
                      "tools/pmc_summary.py",
+           "calib_factor": cf, "calib_source": cf_src,
            "definitions": {
                "clock_ghz": "GRBM_GUI_ACTIVE / 8 XCDs / kernel ns",
-               "valu_instr_per_block": "SQ_INSTS_VALU x 64 lanes / 64-byte blocks (lane-instructions per block)",
+               "valu_instr_per_block": "SQ_INSTS_VALU x 64 lanes / 64-byte blocks hashed (lane-instructions "
+                                       "per block; the step's hash kernels)",
                "simd_cycles_per_valu_instr": "clock cycles x 1024 SIMDs / SQ_INSTS_VALU",
                "valu_busy_pct": "VALUBusy = 100 x SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8)",
+               "valu_busy_pct_own_cus": "heads (one workgroup per CU): the same over the CUs the kernel holds "
+                                        "(SQ_WAVES / waves per workgroup)",
                "valu_utilization_pct": "VALUUtilization = 100 x SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)",
                "int32_share": "SQ_INSTS_VALU_INT32 / SQ_INSTS_VALU",
-               "algorithmic_tops": "1400 x blocks / kernel ns (bench roofline.achieved); frac vs 78.64 T",
-               "hbm_bytes": "FETCH_SIZE x calib (gfx950 half-count, profiles/r01_traffic.json) + WRITE_SIZE"},
+               "algorithmic_tops": "1400 x hashed blocks / kernel ns (bench roofline.achieved); frac vs 78.64 T",
+               "hbm_bytes": "FETCH_SIZE x calib_factor (gfx950 half-count) + WRITE_SIZE, per kernel; the step's "
+                            "is the sum over its kernels"},
            "configs": {}}
     for nm in names:
-        sq, dsq = counters(nm + "_sq")
-        sq2, dsq2 = counters(nm + "_sq2")
-        fe, dfe = counters(nm + "_fetch")
-        wr, dwr = counters(nm + "_write")
+        sq = counters(nm + "_sq")
+        if not sq:
+            continue
+        sq2 = counters(nm + "_sq2")
+        fe = counters(nm + "_fetch")
+        wr = counters(nm + "_write")
         b = bench_line(nm + "_sq")
-        blocks, msgs = b["config"]["blocks_per_gpu"], b["config"]["messages_per_gpu"]
-        grbm, ns = mean_timed(sq, dsq, "GRBM_GUI_ACTIVE")
-        insts, _ = mean_timed(sq, dsq, "SQ_INSTS_VALU")
-        active, _ = mean_timed(sq, dsq, "SQ_ACTIVE_INST_VALU")
-        salu, _ = mean_timed(sq, dsq, "SQ_INSTS_SALU")
-        wave_cyc, _ = mean_timed(sq, dsq, "SQ_WAVE_CYCLES")
-        wait_any, _ = mean_timed(sq, dsq, "SQ_WAIT_ANY")
-        cyc = grbm / XCDS
-        e = {"kernel": kernel_name(nm + "_sq"), "workload": b["config"]["workload"],
-             "messages": msgs, "blocks": blocks, "kernel_us": ns / 1e3,
-             "clock_ghz": cyc / ns,
-             "valu_instr_per_block": insts * 64 / blocks,
-             "salu_instr_per_block": salu * 64 / blocks,
-             "simd_cycles_per_valu_instr": cyc * SIMDS / insts,
-             "valu_busy_pct": 100 * active / CUS / cyc,
-             "wait_any_share": wait_any / wave_cyc if wave_cyc else None,
-             "algorithmic_tops": OPS_PER_BLOCK * blocks / ns / 1e3,
-             "roofline_frac": OPS_PER_BLOCK * blocks / ns / 1e3 / PEAK_TOPS}
-        if sq2:
-            i32, _ = mean_timed(sq2, dsq2, "SQ_INSTS_VALU_INT32")
-            iops, ns2 = mean_timed(sq2, dsq2, "SQ_INSTS_VALU_IOPS")
-            thr, _ = mean_timed(sq2, dsq2, "SQ_THREAD_CYCLES_VALU")
-            act2, _ = mean_timed(sq2, dsq2, "SQ_ACTIVE_INST_VALU")
-            lds, _ = mean_timed(sq2, dsq2, "SQ_INSTS_LDS")
-            e.update({"int32_share": i32 / insts if insts else None,
-                      "valu_iops_counter_T_per_s": iops / ns2 / 1e3,
-                      "valu_utilization_pct": 100 * thr / (act2 * 64) if act2 else None,
-                      "lds_instr_per_block": lds * 64 / blocks})
-        if fe and wr:
-            fetch_kb, _ = mean_timed(fe, dfe, "FETCH_SIZE")
-            write_kb, _ = mean_timed(wr, dwr, "WRITE_SIZE")
-            hbm = fetch_kb * 1024 * cf + write_kb * 1024
+        cfg = b["config"]
+        blocks, msgs = cfg["blocks_per_gpu"], cfg["messages_per_gpu"]
+        hashed = cfg.get("hashed_blocks_per_gpu", blocks)
+        kernels = {k: kernel_entry(k, sq, sq2, fe, wr, cf) for k in sq}
+        hash_k = [k for k in kernels if "k_digest" in k]
+        dom = max(hash_k, key=lambda k: kernels[k]["us"]) if hash_k else max(kernels, key=lambda k: kernels[k]["us"])
+        step_us = sum(e["us"] for e in kernels.values())
+        hash_instr = sum(kernels[k]["valu_lane_instr"] for k in hash_k)
+        d = kernels[dom]
+        e = {"kernel": dom, "workload": cfg["workload"], "messages": msgs, "blocks": blocks,
+             "hashed_blocks": hashed, "kernel_us": d["us"], "clock_ghz": d["clock_ghz"],
+             "valu_instr_per_block": hash_instr / hashed,
+             "simd_cycles_per_valu_instr": d["simd_cycles_per_valu_instr"],
+             "valu_busy_pct": d["valu_busy_pct"], "wait_any_share": d["wait_any_share"],
+             "int32_share": d.get("int32_share"), "valu_utilization_pct": d.get("valu_utilization_pct"),
+             "algorithmic_tops": OPS_PER_BLOCK * hashed / step_us / 1e6,
+             "roofline_frac": OPS_PER_BLOCK * hashed / step_us / 1e6 / PEAK_TOPS,
+             "step": {"us_serialized": step_us, "kernels": sorted(kernels, key=lambda k: -kernels[k]["us"])},
+             "kernels": kernels}
+        if all("hbm_bytes" in k for k in kernels.values()):
+            hbm = sum(k["hbm_bytes"] for k in kernels.values())
             alg = b["roofline"]["algorithmic_bytes_per_launch"]
             e.update({"hbm_bytes": hbm, "algorithmic_bytes": alg, "hbm_over_algorithmic": hbm / alg,
-                      "hbm_gbs": hbm / ns, "hbm_frac_of_8TBs": hbm / ns / HBM_PEAK_GBS})
+                      "hbm_gbs": hbm / (step_us * 1e3), "hbm_frac_of_8TBs": hbm / (step_us * 1e3) / HBM_PEAK_GBS})
         out["configs"][nm] = e
     with open(DST, "w") as f:
         json.dump(out, f, indent=1)
     for nm, e in out["configs"].items():
-        print(f"{nm:24s} {e['kernel_us']:9.1f} us  clk {e['clock_ghz']:.2f}  "
-              f"valu/blk {e['valu_instr_per_block']:7.0f}  cyc/instr {e['simd_cycles_per_valu_instr']:.2f}  "
-              f"busy {e['valu_busy_pct']:5.1f}%  util {e.get('valu_utilization_pct') or 0:5.1f}%  "
-              f"int32 {e.get('int32_share') or 0:.2f}  frac {e['roofline_frac']:.3f}  "
-              f"hbm {e.get('hbm_gbs', 0):6.0f} GB/s x{e.get('hbm_over_algorithmic', 0):.2f}")
+        print(f"{nm:20s} {e['kernel'][:34]:34s} {e['kernel_us']:9.1f} us step {e['step']['us_serialized']:9.1f}"
+              f"  clk {e['clock_ghz'] or 0:.2f}  valu/blk {e['valu_instr_per_block']:7.0f}"
+              f"  cyc/instr {e['simd_cycles_per_valu_instr'] or 0:.2f}  busy {e['valu_busy_pct'] or 0:5.1f}%"
+              f"  frac {e['roofline_frac']:.3f}  hbm x{e.get('hbm_over_algorithmic', 0):.2f}")
+        for k, v in e["kernels"].items():
+            if k != e["kernel"]:
+                own = v.get("valu_busy_pct_own_cus")
+                print(f"    {k[:44]:44s} {v['us']:8.1f} us  busy {v['valu_busy_pct'] or 0:5.1f}%"
+                      + (f" (own CUs {own:5.1f}%, {v['occupied_cus']:.0f} CUs)" if own is not None else "")
+                      + f"  hbm {v.get('hbm_bytes', 0) / 1e6:8.1f} MB")
 
 
 if __name__ == "__main__":

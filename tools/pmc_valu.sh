@@ -5,7 +5,7 @@
 #   fetch : FETCH_SIZE        write : WRITE_SIZE   (HBM bytes, gfx950 recipe)
 #   ifetch: instruction cache (SQC_ICACHE_*), instruction-issue waits, instruction fetches
 # -> gpurun_out/pmc/<cfg>_<pass>/run_counter_collection.csv; summarise with
-#    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r01_pmc.json
+#    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r04_pmc.json
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/pmc
@@ -20,8 +20,13 @@ SQ2="SQ_INSTS_VALU_INT32 SQ_INSTS_VALU_IOPS SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST
 IF="SQC_ICACHE_REQ SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE SQ_WAIT_INST_ANY SQ_WAVE_CYCLES SQ_IFETCH SQ_INSTS_VALU GRBM_GUI_ACTIVE"
 PASSES=${PASSES:-sq sq2 fetch write}
 has() { [[ " $PASSES " == *" $1 "* ]]; }
-for spec in ${SPECS:-c2:auto c3:auto c3dd:auto c4:auto c5:auto ub_16384_65536:coop ub_16384_65536:lane}; do
-  cfg=${spec%%:*}; pol=${spec##*:}; arg=$(echo $cfg | tr '_' ':')
+# FETCH_SIZE calibration of this box (tools/traffic_calib, built on the CPU side)
+if has fetch && [ -x tools/traffic_calib ] && [ -z "${NO_CALIB:-}" ]; then
+  prof calib_fetch FETCH_SIZE ./tools/traffic_calib
+fi
+for spec in ${SPECS:-c2:auto c3:auto c3dd:auto c4:auto c5:auto c5_planned:auto c5_folded:auto}; do
+  cfg=${spec%%:*}; pol=${spec##*:}; arg=$cfg
+  case $cfg in ub_*|u_*) arg=$(echo $cfg | tr '_' ':') ;; esac
   name=${cfg}_${pol}
   cmd="python3 bench.py --config $arg --policy $pol --steps 3 --warmup 1 --no-cpu-baseline --no-extra --no-host-api"
   has sq && prof ${name}_sq "$SQ" $cmd
