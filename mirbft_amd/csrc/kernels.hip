@@ -893,13 +893,30 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
                  : "+v"(t_) : "v"(W), "v"(u_));                                                  \
     W = t_;                                                                                      \
   }
-#define MSHA_D4(q)                                 \
+// Four rounds from quad q of cur; the same quad of the NEXT block is read from
+// LDS slot nxt meanwhile, so its latency hides under the rounds.
+#define MSHA_D4(cur, nxt, q)                       \
   {                                                \
-    const uint4 v_ = kv[q];                        \
+    const uint4 v_ = cur[q];                       \
+    nxt[q] = kw[ns][col + (q) * qstride];          \
     MSHA_DROUND(X, Y, Z, W, v_.x)                  \
     MSHA_DROUND(W, X, Y, Z, v_.y)                  \
     MSHA_DROUND(Z, W, X, Y, v_.z)                  \
     MSHA_DROUND(Y, Z, W, X, v_.w)                  \
+  }
+// One block b from cur (read during the previous block), reading block b+1's
+// K+W (slot ns) into nxt; the digest is stored after the message's last block.
+#define MSHA_DBLOCK(cur, nxt)                                                                          \
+  {                                                                                                    \
+    uint32_t X = H0, Y = H1, Z = H2, W = H3;                                                           \
+    MSHA_D4(cur, nxt, 0) MSHA_D4(cur, nxt, 1) MSHA_D4(cur, nxt, 2) MSHA_D4(cur, nxt, 3)              \
+    MSHA_D4(cur, nxt, 4) MSHA_D4(cur, nxt, 5) MSHA_D4(cur, nxt, 6) MSHA_D4(cur, nxt, 7)              \
+    MSHA_D4(cur, nxt, 8) MSHA_D4(cur, nxt, 9) MSHA_D4(cur, nxt, 10) MSHA_D4(cur, nxt, 11)            \
+    MSHA_D4(cur, nxt, 12) MSHA_D4(cur, nxt, 13) MSHA_D4(cur, nxt, 14) MSHA_D4(cur, nxt, 15)          \
+    H0 += X; H1 += Y; H2 += Z; H3 += W;                                                                \
+    if (active && b + 1 == nb)                                                                         \
+      *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =                                     \
+          make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));                                      \
   }
 
 // Also AUTO's kernel for launches of at most 64 messages per CU (a call of a
@@ -973,8 +990,9 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
       }
       if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
       schedule_kw(w, &kw[b & 1][lane]);
-      __syncthreads();
+      __syncthreads();  // barrier b: slot b & 1 holds block b
     }
+    __syncthreads();  // barrier NB: the consumers' last (they wait one block ahead)
   } else {
     // e-side: e f g h, rotates 6 11 25; a-side: a b c d, rotates 2 13 22
     uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
@@ -982,21 +1000,29 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     const uint32_t sh1 = eside ? 6 : 2, sh2 = eside ? 11 : 13, sh3 = eside ? 25 : 22;
     const unsigned col = eside ? msg : kCoopSlotQuads * 64;  // a-lanes read the zero quads
     const unsigned qstride = eside ? 64 : 1;
-    for (uint32_t b = 0; b < NB; ++b) {
-      __syncthreads();
-      uint4 kv[16];
+    // Block b's K+W is read from LDS during block b-1's rounds (MSHA_D4), so a
+    // block starts on registers: barrier b+1 (the producer has written slot
+    // (b+1) & 1) opens block b, whose rounds read it. The producer fills slot
+    // b+2 -- the one block b-1 read, complete at barrier b+1 (__syncthreads
+    // waits for every outstanding LDS read) -- while block b computes. Two
+    // register sets alternate by unrolling the block loop twice, so nothing is
+    // copied between blocks.
+    uint4 ka[16], kb[16];
+    __syncthreads();  // barrier 0: slot 0 holds block 0
 #pragma unroll
-      for (int q = 0; q < 16; ++q) kv[q] = kw[b & 1][col + q * qstride];
-      uint32_t X = H0, Y = H1, Z = H2, W = H3;
-      MSHA_D4(0) MSHA_D4(1) MSHA_D4(2) MSHA_D4(3) MSHA_D4(4) MSHA_D4(5) MSHA_D4(6) MSHA_D4(7)
-      MSHA_D4(8) MSHA_D4(9) MSHA_D4(10) MSHA_D4(11) MSHA_D4(12) MSHA_D4(13) MSHA_D4(14) MSHA_D4(15)
-      H0 += X; H1 += Y; H2 += Z; H3 += W;
-      if (active && b + 1 == nb)
-        *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =
-            make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));
+    for (int q = 0; q < 16; ++q) ka[q] = kw[0][col + q * qstride];
+    for (uint32_t b = 0; b < NB; ++b) {
+      __syncthreads();  // barrier b+1
+      unsigned ns = (b + 1) & 1;  // a read past the last block is harmless (unused)
+      MSHA_DBLOCK(ka, kb)
+      if (++b == NB) break;
+      __syncthreads();  // barrier b+1
+      ns = (b + 1) & 1;
+      MSHA_DBLOCK(kb, ka)
     }
   }
 }
+#undef MSHA_DBLOCK
 #undef MSHA_D4
 #undef MSHA_DROUND
 
