@@ -51,6 +51,7 @@ import (
 
 	"github.com/pkg/errors"
 
+	"github.com/hyperledger-labs/mirbft/pkg/pb/msgs"
 	"github.com/hyperledger-labs/mirbft/pkg/pb/state"
 	"github.com/hyperledger-labs/mirbft/pkg/statemachine"
 )
@@ -116,6 +117,26 @@ func (g *GPUHasher) fail(rc C.int) error {
 	return errors.Errorf("libmirsha error %d: %s", int(rc), C.GoString(&buf[0]))
 }
 
+// lastPayloadUpload is the payload bytes the last call uploaded, summed over
+// the context's GPUs (msha_get_shard_stats.h2d_payload_bytes; for tests).
+func (g *GPUHasher) lastPayloadUpload() (uint64, error) {
+	g.mutex.Lock()
+	defer g.mutex.Unlock()
+	var n C.uint32_t
+	if rc := C.msha_shard_count(g.ctx, &n); rc != C.MSHA_OK {
+		return 0, g.fail(rc)
+	}
+	total := uint64(0)
+	for i := C.uint32_t(0); i < n; i++ {
+		var st C.msha_shard_stats
+		if rc := C.msha_get_shard_stats(g.ctx, i, &st); rc != C.MSHA_OK {
+			return 0, g.fail(rc)
+		}
+		total += uint64(st.h2d_payload_bytes)
+	}
+	return total, nil
+}
+
 // ensure returns p's buffer resized to n bytes (grown in pinned memory on demand).
 func (g *GPUHasher) ensure(p *pinnedBuf, n int) ([]byte, error) {
 	if cap(p.buf) >= n {
@@ -146,12 +167,16 @@ func (g *GPUHasher) words(p *pinnedBuf, n int) ([]uint64, error) {
 }
 
 // digests hashes n messages in one msha_digest_batch call. size bounds the
-// packed arena (every message's bytes plus up to 15 bytes of alignment); pack(i,
-// dst) copies message i's bytes to dst and returns their count. Messages are
+// packed arena (every packed message's bytes plus up to 15 bytes of alignment);
+// pack(i, dst) copies message i's bytes to dst and returns their count. alias
+// (nil, or one entry per message) names, for a message whose bytes equal an
+// earlier message's, that earlier message (else -1): it is not packed again but
+// gets the same (off, len), so its payload crosses PCIe once and the library
+// hashes it once (msha_digest_batch folds equal (off, len)). Messages are
 // placed 16-byte aligned and the arena, offsets, lengths and digests all live in
 // pinned memory, so the library DMAs them as they are (no staging copy) and
 // plans the lanes on the GPU. Returns n fresh 32-byte digests.
-func (g *GPUHasher) digests(n int, size int, pack func(i int, dst []byte) int) ([][]byte, error) {
+func (g *GPUHasher) digests(n int, size int, pack func(i int, dst []byte) int, alias []int) ([][]byte, error) {
 	g.mutex.Lock()
 	defer g.mutex.Unlock()
 	if g.ctx == nil {
@@ -179,6 +204,10 @@ func (g *GPUHasher) digests(n int, size int, pack func(i int, dst []byte) int) (
 	}
 	pos := 0
 	for i := 0; i < n; i++ {
+		if alias != nil && alias[i] >= 0 {
+			off[i], length[i] = off[alias[i]], length[alias[i]]
+			continue
+		}
 		off[i] = uint64(pos)
 		l := pack(i, arena[pos:])
 		length[i] = uint64(l)
@@ -199,35 +228,121 @@ func (g *GPUHasher) digests(n int, size int, pack func(i int, dst []byte) int) (
 	return result, nil
 }
 
+// partsLen is the length of the concatenation of parts.
+func partsLen(parts [][]byte) int {
+	n := 0
+	for _, p := range parts {
+		n += len(p)
+	}
+	return n
+}
+
+// partsEqual reports whether two part lists concatenate to the same bytes
+// (their part boundaries may differ).
+func partsEqual(a, b [][]byte) bool {
+	var x, y []byte
+	for {
+		for len(x) == 0 && len(a) > 0 {
+			x, a = a[0], a[1:]
+		}
+		for len(y) == 0 && len(b) > 0 {
+			y, b = b[0], b[1:]
+		}
+		if len(x) == 0 || len(y) == 0 {
+			return len(x) == 0 && len(y) == 0
+		}
+		k := len(x)
+		if len(y) < k {
+			k = len(y)
+		}
+		if string(x[:k]) != string(y[:k]) {
+			return false
+		}
+		x, y = x[k:], y[k:]
+	}
+}
+
+// epochChangeAliases finds the EpochChange hash actions whose payload an
+// earlier action of the list already carries. A node hashes every origin's
+// EpochChange once per ack (epoch_target.go:486-528, epoch_tracker.go:349-350):
+// N^2 requests over N distinct payloads per epoch change. In the testengine
+// the acks hold the originator's *msgs.EpochChange by pointer (recorder.go:39-47),
+// so a pointer seen before is the same payload; acks deserialized from the
+// network hold equal copies, found by comparing the bytes of earlier payloads
+// from the same origin node with the same length (a byzantine copy that differs
+// is packed and hashed on its own). alias[i] = that earlier action, or -1.
+func epochChangeAliases(reqs []*state.ActionHashRequest) (alias []int, size int) {
+	type contentKey struct {
+		origin uint64
+		length int
+	}
+	alias = make([]int, len(reqs))
+	var byPtr map[*msgs.EpochChange]int
+	var byContent map[contentKey][]int
+	for i, r := range reqs {
+		alias[i] = -1
+		l := partsLen(r.Data)
+		if t, ok := r.Origin.GetType().(*state.HashOrigin_EpochChange_); ok && t.EpochChange != nil {
+			ec := t.EpochChange
+			if byPtr == nil {
+				byPtr = map[*msgs.EpochChange]int{}
+				byContent = map[contentKey][]int{}
+			}
+			if j, seen := byPtr[ec.EpochChange]; seen && ec.EpochChange != nil {
+				alias[i] = j
+				continue
+			}
+			k := contentKey{ec.Origin, l}
+			for _, j := range byContent[k] {
+				if partsEqual(reqs[j].Data, r.Data) {
+					alias[i] = j
+					break
+				}
+			}
+			if ec.EpochChange != nil {
+				if alias[i] >= 0 {
+					byPtr[ec.EpochChange] = alias[i]
+				} else {
+					byPtr[ec.EpochChange] = i
+				}
+			}
+			if alias[i] >= 0 {
+				continue
+			}
+			byContent[k] = append(byContent[k], i)
+		}
+		size += l + 15
+	}
+	return alias, size
+}
+
 // ProcessHashActionsGPU is a drop-in for ProcessHashActions (serial.go:180-198):
 // one HashResult per action, in input order, Digest = SHA-256 of the action's
 // Data parts concatenated (h.Write appends; zero parts hash the empty string),
 // Origin the same pointer as the action's; a non-hash action fails the whole
-// list with the reference's error text. One libmirsha call per ActionList.
+// list with the reference's error text. One libmirsha call per ActionList; an
+// EpochChange payload the list already carries is packed once and shared
+// (epochChangeAliases).
 func ProcessHashActionsGPU(g *GPUHasher, actions *statemachine.ActionList) (*statemachine.EventList, error) {
 	reqs := make([]*state.ActionHashRequest, 0, actions.Len())
-	size := 0
 	iter := actions.Iterator()
 	for action := iter.Next(); action != nil; action = iter.Next() {
 		switch t := action.Type.(type) {
 		case *state.Action_Hash:
 			reqs = append(reqs, t.Hash)
-			for _, data := range t.Hash.Data {
-				size += len(data)
-			}
-			size += 15
 		default:
 			return nil, errors.Errorf("unexpected type for Hash action: %T", action.Type)
 		}
 	}
 
+	alias, size := epochChangeAliases(reqs)
 	digests, err := g.digests(len(reqs), size, func(i int, dst []byte) int {
 		n := 0
 		for _, data := range reqs[i].Data {
 			n += copy(dst[n:], data)
 		}
 		return n
-	})
+	}, alias)
 	if err != nil {
 		return nil, err
 	}
@@ -248,5 +363,5 @@ func (g *GPUHasher) RequestDigests(reqs []ProposedRequest) ([][]byte, error) {
 	}
 	return g.digests(len(reqs), size, func(i int, dst []byte) int {
 		return copy(dst, reqs[i].Data)
-	})
+	}, nil)
 }

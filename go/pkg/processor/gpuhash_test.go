@@ -18,6 +18,8 @@ import (
 	"strings"
 	"testing"
 
+	"google.golang.org/protobuf/proto"
+
 	"github.com/hyperledger-labs/mirbft/pkg/pb/msgs"
 	"github.com/hyperledger-labs/mirbft/pkg/pb/state"
 	"github.com/hyperledger-labs/mirbft/pkg/statemachine"
@@ -95,6 +97,80 @@ func TestGPUProcessHashActionsMatchesReference(t *testing.T) {
 		if e.HashResult.Origin != a.Type.(*state.Action_Hash).Hash.Origin {
 			t.Errorf("action %d: origin is not the action's pointer", i)
 		}
+	}
+}
+
+// ecHashData restates epochChangeHashData (stateless.go:323-352, unexported
+// in package statemachine): [BE64(new_epoch)] ++ [BE64(seq), value] per
+// checkpoint ++ [BE64(epoch), BE64(seq), digest] per P and Q entry.
+func ecHashData(ec *msgs.EpochChange) [][]byte {
+	data := [][]byte{be64(ec.NewEpoch)}
+	for _, cp := range ec.Checkpoints {
+		data = append(data, be64(cp.SeqNo), cp.Value)
+	}
+	for _, set := range [][]*msgs.EpochChange_SetEntry{ec.PSet, ec.QSet} {
+		for _, e := range set {
+			data = append(data, be64(e.Epoch), be64(e.SeqNo), e.Digest)
+		}
+	}
+	return data
+}
+
+// An epoch-change storm (epoch_target.go:486-528): every node hashes each of N
+// origins' EpochChange once per ack. Acks of the testengine carry the
+// originator's message by pointer; acks off the wire carry equal copies; a
+// byzantine forwarder may carry an altered one. ProcessHashActionsGPU packs
+// each distinct payload once and must still return the reference's digest for
+// every action, altered copies included.
+func TestGPUEpochChangeStormPackedOnce(t *testing.T) {
+	g := newGPU(t)
+	defer g.Close()
+	const nodes = 16
+	al := &statemachine.ActionList{}
+	distinct := 0
+	for o := 0; o < nodes; o++ {
+		ec := &msgs.EpochChange{NewEpoch: 7, Checkpoints: []*msgs.Checkpoint{
+			{SeqNo: 500, Value: bytes.Repeat([]byte{byte(o)}, 332)}, {SeqNo: 1000, Value: bytes.Repeat([]byte{byte(o + 1)}, 332)}}}
+		for s := 0; s < 300+40*o; s++ {
+			ec.PSet = append(ec.PSet, &msgs.EpochChange_SetEntry{Epoch: 6, SeqNo: uint64(s), Digest: bytes.Repeat([]byte{byte(s)}, 32)})
+		}
+		distinct += partsLen(ecHashData(ec))
+		for src := 0; src < nodes; src++ {
+			msg := ec // by pointer (the testengine)
+			if src%3 == 1 {
+				msg = proto.Clone(ec).(*msgs.EpochChange) // an equal copy (off the wire)
+			}
+			al.Hash(ecHashData(msg), &state.HashOrigin{Type: &state.HashOrigin_EpochChange_{
+				EpochChange: &state.HashOrigin_EpochChange{Source: uint64(src), Origin: uint64(o), EpochChange: msg}}})
+		}
+		bad := proto.Clone(ec).(*msgs.EpochChange) // same origin, same length, one byte differs
+		bad.PSet[0].Digest = bytes.Repeat([]byte{0xEE}, 32)
+		distinct += partsLen(ecHashData(bad))
+		al.Hash(ecHashData(bad), &state.HashOrigin{Type: &state.HashOrigin_EpochChange_{
+			EpochChange: &state.HashOrigin_EpochChange{Source: 99, Origin: uint64(o), EpochChange: bad}}})
+	}
+	want, err := ProcessHashActions(crypto.SHA256, al)
+	if err != nil {
+		t.Fatal(err)
+	}
+	got, err := ProcessHashActionsGPU(g, al)
+	if err != nil {
+		t.Fatal(err)
+	}
+	wi, gi := want.Iterator(), got.Iterator()
+	for i := 0; i < want.Len(); i++ {
+		w, e := wi.Next().Type.(*state.Event_HashResult), gi.Next().Type.(*state.Event_HashResult)
+		if !bytes.Equal(w.HashResult.Digest, e.HashResult.Digest) {
+			t.Fatalf("action %d: digest %x, want %x", i, e.HashResult.Digest, w.HashResult.Digest)
+		}
+	}
+	up, err := g.lastPayloadUpload()
+	if err != nil {
+		t.Fatal(err)
+	}
+	// each distinct payload once (plus its 16-byte alignment), not nodes times
+	if up < uint64(distinct) || up > uint64(distinct+16*2*nodes) {
+		t.Fatalf("uploaded %d payload bytes, distinct payloads hold %d", up, distinct)
 	}
 }
 

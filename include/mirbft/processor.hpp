@@ -21,6 +21,7 @@
 
 #include <cstdint>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -49,7 +50,10 @@ struct HashOriginVerifyBatch {
   Bytes expected_digest;
 };
 struct HashOriginEpochChange {
-  uint64_t source = 0, origin = 0;  // epoch_change payload omitted: only its hash data matters here
+  uint64_t source = 0, origin = 0;
+  // The *msgs.EpochChange the hash data was built from, by identity only (its
+  // fields are not needed here): actions sharing one message share a payload.
+  std::shared_ptr<const void> epoch_change;
 };
 struct HashOrigin {
   std::variant<std::monostate, HashOriginBatch, HashOriginEpochChange, HashOriginVerifyBatch> type;
@@ -158,11 +162,16 @@ class GPUHasher {
   // parts are packed back to back (h.Write appends), every message starting
   // 16-byte aligned, into the context's pinned arena: libmirsha uploads it as
   // is (msha_pinned_alloc / msha_stats.direct_calls), one msha_digest_batch.
-  Result<std::vector<Bytes>> HashBatch(const std::vector<const std::vector<Bytes>*>& msgs) {
+  // alias (optional, one entry per message): an earlier message with the same
+  // bytes, or -1; such a message is not packed again but shares that one's
+  // (off, len), so its payload crosses PCIe once.
+  Result<std::vector<Bytes>> HashBatch(const std::vector<const std::vector<Bytes>*>& msgs,
+                                       const std::vector<int64_t>* alias = nullptr) {
     Result<std::vector<Bytes>> r;
     size_t n_bytes = 0;
-    for (auto* m : msgs) {
-      for (auto& p : *m) n_bytes += p.size();
+    for (size_t i = 0; i < msgs.size(); ++i) {
+      if (alias && (*alias)[i] >= 0) continue;
+      for (auto& p : *msgs[i]) n_bytes += p.size();
       n_bytes += 15;
     }
     std::vector<uint64_t> off(msgs.size() + 1), len(msgs.size() + 1);
@@ -170,6 +179,11 @@ class GPUHasher {
     if (!PinnedArena(n_bytes + 64, &arena, &r.err)) return r;
     size_t pos = 0;
     for (size_t i = 0; i < msgs.size(); ++i) {
+      if (alias && (*alias)[i] >= 0) {
+        off[i] = off[(*alias)[i]];
+        len[i] = len[(*alias)[i]];
+        continue;
+      }
       off[i] = pos;
       for (auto& p : *msgs[i]) {
         if (!p.empty()) std::memcpy(arena + pos, p.data(), p.size());
@@ -243,6 +257,46 @@ inline Bytes GPUHash::Sum(Bytes b) const {
   return b;
 }
 
+// The Go drop-in's epochChangeAliases (gpuhash.go): alias[i] = an earlier
+// request carrying request i's EpochChange payload, else -1. Each origin's
+// EpochChange is hashed once per ack (epoch_target.go:486-528): the same
+// message object is the same payload (the testengine passes it by pointer,
+// recorder.go:39-47); an equal payload from the same origin node with the same
+// length (an ack off the wire) is found by comparing bytes; an altered copy is
+// packed and hashed on its own.
+inline std::vector<int64_t> EpochChangeAliases(const std::vector<const ActionHashRequest*>& reqs) {
+  std::vector<int64_t> alias(reqs.size(), -1);
+  std::map<const void*, int64_t> by_obj;
+  std::map<std::pair<uint64_t, size_t>, std::vector<int64_t>> by_content;
+  auto concat = [](const std::vector<Bytes>& parts) {
+    Bytes b;
+    for (auto& p : parts) b.insert(b.end(), p.begin(), p.end());
+    return b;
+  };
+  for (size_t i = 0; i < reqs.size(); ++i) {
+    const auto* o = reqs[i]->origin ? std::get_if<HashOriginEpochChange>(&reqs[i]->origin->type) : nullptr;
+    if (!o) continue;
+    const void* key = o->epoch_change.get();
+    if (key) {
+      auto it = by_obj.find(key);
+      if (it != by_obj.end()) {
+        alias[i] = it->second;
+        continue;
+      }
+    }
+    const Bytes mine = concat(reqs[i]->data);
+    auto& cands = by_content[{o->origin, mine.size()}];
+    for (int64_t j : cands)
+      if (concat(reqs[j]->data) == mine) {
+        alias[i] = j;
+        break;
+      }
+    if (key) by_obj[key] = alias[i] >= 0 ? alias[i] : (int64_t)i;
+    if (alias[i] < 0) cands.push_back((int64_t)i);
+  }
+  return alias;
+}
+
 // processor.ProcessHashActions (serial.go:180-198), one GPU batch per list.
 inline Result<statemachine::EventList> ProcessHashActions(GPUHasher& hasher,
                                                           const statemachine::ActionList& actions) {
@@ -260,7 +314,8 @@ inline Result<statemachine::EventList> ProcessHashActions(GPUHasher& hasher,
   std::vector<const std::vector<Bytes>*> msgs;
   msgs.reserve(reqs.size());
   for (auto* q : reqs) msgs.push_back(&q->data);
-  auto digests = hasher.HashBatch(msgs);
+  const std::vector<int64_t> alias = EpochChangeAliases(reqs);
+  auto digests = hasher.HashBatch(msgs, &alias);
   if (!digests.ok()) {
     r.err = digests.err;
     return r;

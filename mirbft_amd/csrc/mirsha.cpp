@@ -1018,16 +1018,21 @@ struct SmallSpan {
   uint64_t lo, hi;
 };
 
+// first (may be null): first[i] = the earliest message with message i's (off,
+// len) (alias_uids): an aliased payload is packed once and its aliases point at
+// it (EpochChange re-hashes, epoch_target.go:486-505; the Go adapter shares a
+// payload between actions, gpuhash.go epochChangeAliases).
 template <class Fill>
 void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_t* out, Fill&& fill,
-               const SmallSpan* span = nullptr) {
+               const SmallSpan* span = nullptr, const uint64_t* first = nullptr) {
   Device& d = ctx->devs[0];
   const uint64_t meta = (16 * m + 63) & ~uint64_t(63);  // off[m], len[m]; payload 64-B aligned after
   uint64_t pay = 0;
   if (span) {
     pay = span->hi - span->lo;
   } else {
-    for (uint64_t i = 0; i < m; ++i) pay += round16(len[i]);
+    for (uint64_t i = 0; i < m; ++i)
+      if (!first || first[i] == i) pay += round16(len[i]);
   }
   d.sm_stage.ensure(meta + (span ? 0 : pay));
   uint64_t* h_off = d.sm_stage.as<uint64_t>();
@@ -1038,6 +1043,8 @@ void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_
     h_len[i] = len[i];
     if (span) {
       h_off[i] = span->off[i] - span->lo;
+    } else if (first && first[i] != i) {
+      h_off[i] = h_off[first[i]];
     } else {
       h_off[i] = a;
       if (len[i]) fill(i, h_pay + a);
@@ -2223,12 +2230,28 @@ int msha_digest_batch(msha_ctx* ctx, const uint8_t* arena, uint64_t arena_len, c
       const bool span = small_bytes() > 0 && aligned16 && hi - lo > kSmallSpanMin &&
                         hi - lo <= small_span_bytes() && is_pinned_host(arena + lo) &&
                         is_pinned_host(arena + hi - 1);
+      // Packed, an aliased payload goes up once: offsets that strictly increase
+      // cannot repeat a payload (the common case, one pass); otherwise the
+      // host's alias detection names each message's first.
       uint64_t packed = 0;
-      for (uint64_t i = 0; i < n && !span; ++i) packed += round16(len[i]);
+      bool increasing = true;
+      for (uint64_t i = 0; i < n && !span; ++i) {
+        packed += round16(len[i]);
+        increasing = increasing && (i == 0 || off[i] > off[i - 1]);
+      }
+      std::vector<uint64_t> first;
+      if (!span && !increasing) {
+        std::vector<uint64_t> table, bucket;
+        std::vector<uint32_t> tag;
+        alias_uids(off, len, n, first, table, bucket, tag);
+        packed = 0;
+        for (uint64_t i = 0; i < n; ++i)
+          if (first[i] == i) packed += round16(len[i]);
+      }
       if (span || small_call(n, packed)) {
         const SmallSpan sp{arena, off, lo, hi};
         run_small(ctx, t0, n, len, out, [&](uint64_t i, uint8_t* dst) { std::memcpy(dst, arena + off[i], len[i]); },
-                  span ? &sp : nullptr);
+                  span ? &sp : nullptr, first.empty() ? nullptr : first.data());
         ctx->stats.direct_calls += span;
         count();
         return;

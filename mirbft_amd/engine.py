@@ -106,6 +106,13 @@ class Engine:
         buf = (ctypes.c_uint8 * max(int(nbytes), 1)).from_address(p.value)
         return np.frombuffer(buf, dtype=np.uint8, count=int(nbytes))
 
+    def pinned_free(self, a: np.ndarray) -> None:
+        """Release a buffer from pinned_empty (by its base address)."""
+        addr = a.__array_interface__["data"][0]
+        if addr in getattr(self, "_pinned", []):
+            self._pinned.remove(addr)
+            self._check(self._lib.msha_pinned_free(self._ctx, addr))
+
     def __enter__(self):
         return self
 

@@ -16,6 +16,11 @@ it fail with "unexpected type for Hash action: <type>" (serial.go:192-194),
 raised here as ``ProcessorError``. The whole list is hashed by ONE
 ``msha_hash_actions`` call (one H2D, one launch per GPU, one D2H).
 
+An EpochChange payload the list already carries is packed once (as the Go
+drop-in does, go/pkg/processor/gpuhash.go epochChangeAliases): actions whose
+origin holds the same EpochChange object, or an equal payload from the same
+origin node, share the first one's (off, len), so it crosses PCIe once.
+
 ``GPUHasher.new()`` keeps the per-message ``hash.Hash`` surface that
 ``Client.Propose`` (clients.go:189-192) and the testengine app chain
 (recorder.go:288-359) use: writes are buffered and ``sum()`` submits a
@@ -185,6 +190,60 @@ class GPUHasher:
     def hash_batch(self, actions: Sequence[Sequence[bytes]]) -> List[bytes]:
         return self.engine.hash_actions(actions)
 
+    def close(self) -> None:
+        """Release the packing buffers (the engine stays open)."""
+        for name in ("_arena", "_off", "_len", "_out"):
+            buf = self.__dict__.pop(name, None)
+            if buf is not None and getattr(self.engine, "_ctx", None):
+                self.engine.pinned_free(buf)
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _pinned(self, name: str, nbytes: int) -> np.ndarray:
+        """A page-locked buffer of at least nbytes, grown on demand (the Go
+        adapter's pinnedBuf)."""
+        buf = getattr(self, name, None)
+        if buf is None or buf.size < nbytes:
+            if buf is not None:
+                self.engine.pinned_free(buf)
+            buf = self.engine.pinned_empty(max(nbytes + nbytes // 4, 4096))
+            setattr(self, name, buf)
+        return buf[:nbytes]
+
+    def hash_requests(self, reqs: Sequence["ActionHashRequest"]) -> List[bytes]:
+        """One digest per hash request, packed the way the Go drop-in packs an
+        ActionList (gpuhash.go digests): each request's parts back to back,
+        16-byte aligned, in a pinned arena; off/len and the digests pinned
+        too; ONE msha_digest_batch. EpochChange payloads are packed once
+        (_epoch_change_aliases). last_pack holds what was packed."""
+        n = len(reqs)
+        alias = _epoch_change_aliases(reqs)
+        off = self._pinned("_off", 8 * n).view(np.uint64)
+        ln = self._pinned("_len", 8 * n).view(np.uint64)
+        chunks, pos = [], 0
+        for i, r in enumerate(reqs):
+            j = alias[i]
+            if j >= 0:
+                off[i], ln[i] = off[j], ln[j]
+                continue
+            data = b"".join(r.data)
+            off[i], ln[i] = pos, len(data)
+            chunks.append((pos, data))
+            pos = (pos + len(data) + 15) & ~15
+        arena = self._pinned("_arena", pos + 64)
+        for p, data in chunks:
+            arena[p:p + len(data)] = np.frombuffer(data, dtype=np.uint8)
+        out = self._pinned("_out", 32 * n).reshape(n, 32)
+        self.engine.digest_batch(arena, off, ln, out=out)
+        self.last_pack = {"actions": n, "payloads": len(chunks), "packed_bytes": pos,
+                          "payload_bytes": sum(len(d) for _, d in chunks),
+                          "aliased": int(sum(1 for a in alias if a >= 0))}
+        return [bytes(r) for r in out]
+
     def request_digests(self, requests: Sequence[bytes]) -> List[bytes]:
         """Batched request intake: the digest that
         Client.Propose computes per call (clients.go:189-192, ``h.Write(data);
@@ -227,9 +286,41 @@ def checkpoint_hashes(hasher: GPUHasher, intervals: Sequence[tuple]) -> List[byt
     return [bytes(r) for r in out]
 
 
+def _epoch_change_aliases(reqs: Sequence[ActionHashRequest]) -> List[int]:
+    """alias[i] = an earlier request carrying request i's EpochChange payload,
+    else -1 (the Go drop-in's epochChangeAliases, gpuhash.go). Each origin's
+    EpochChange is hashed once per ack (epoch_target.go:486-528,
+    epoch_tracker.go:349-350). The testengine's acks hold the originator's
+    message itself (recorder.go:39-47): the same object is the same payload.
+    Acks off the wire hold equal copies: payloads from the same origin node
+    with the same length are compared byte for byte (an altered copy is packed
+    and hashed on its own)."""
+    alias = [-1] * len(reqs)
+    by_obj: dict = {}       # id(EpochChange) -> request index (objects live as long as reqs)
+    by_content: dict = {}   # (origin node, length) -> [(index, payload)]
+    for i, r in enumerate(reqs):
+        t = r.origin.type if r.origin is not None else None
+        if not isinstance(t, HashOriginEpochChange):
+            continue
+        ec = t.epoch_change
+        if ec is not None and id(ec) in by_obj:
+            alias[i] = by_obj[id(ec)]
+            continue
+        data = b"".join(r.data)
+        key = (t.origin, len(data))
+        match = next((j for j, d in by_content.get(key, ()) if d == data), -1)
+        if ec is not None:
+            by_obj[id(ec)] = match if match >= 0 else i
+        if match >= 0:
+            alias[i] = match
+        else:
+            by_content.setdefault(key, []).append((i, data))
+    return alias
+
+
 def ProcessHashActions(hasher: GPUHasher, actions: ActionList) -> EventList:
     """processor.ProcessHashActions (serial.go:180-198), one GPU batch per list."""
-    if not hasattr(hasher, "hash_batch"):
+    if not hasattr(hasher, "hash_requests"):
         raise TypeError("ProcessHashActions needs a GPU-backed hasher (GPUHasher); "
                         "this engine has no CPU hashing path")
     reqs: List[ActionHashRequest] = []
@@ -238,7 +329,7 @@ def ProcessHashActions(hasher: GPUHasher, actions: ActionList) -> EventList:
         if not isinstance(t, ActionHash):
             raise ProcessorError(f"unexpected type for Hash action: {type(t).__name__}")
         reqs.append(t.hash)
-    digests = hasher.hash_batch([r.data for r in reqs]) if reqs else []
+    digests = hasher.hash_requests(reqs) if reqs else []
     events = EventList()
     for r, d in zip(reqs, digests):
         events.hash_result(d, r.origin)

@@ -130,6 +130,49 @@ int main() {
     for (int i = 0; i < 3000; i += 7)
       EXPECT(r2.value.Items()[i].digest == oracle({Bytes(400 + i % 50, (uint8_t)i), Bytes(i % 13, 9)}), "digest");
   }
+  {  // Describe("epoch-change storm") It("packs each distinct EpochChange payload once")
+     // Every node hashes each origin's EpochChange once per ack (epoch_target.go:486-528):
+     // acks of one message share it (the testengine passes it by pointer), equal copies
+     // off the wire share it by content, an altered copy is hashed on its own.
+    const int nodes = 12;
+    ActionList al;
+    std::vector<std::vector<Bytes>> parts_of;
+    uint64_t distinct = 0;
+    for (int o = 0; o < nodes; ++o) {
+      std::vector<Bytes> data{Bytes(8, (uint8_t)o), Bytes(332, (uint8_t)(o + 1))};
+      for (int e = 0; e < 2000 + 300 * o; ++e) data.push_back(Bytes(48, (uint8_t)(e ^ o)));
+      auto msg = std::make_shared<int>(o);  // the message's identity
+      uint64_t bytes = 0;
+      for (auto& p : data) bytes += p.size();
+      distinct += 2 * ((bytes + 15) / 16 * 16);  // the message and its altered copy
+      for (int src = 0; src < nodes; ++src) {
+        auto origin = std::make_shared<HashOrigin>();
+        HashOriginEpochChange ec{(uint64_t)src, (uint64_t)o, src % 3 == 1 ? std::make_shared<int>(o) : msg};
+        origin->type = ec;
+        al.Hash(data, origin);
+        parts_of.push_back(data);
+      }
+      std::vector<Bytes> bad = data;
+      bad.back()[0] ^= 1;
+      auto origin = std::make_shared<HashOrigin>();
+      origin->type = HashOriginEpochChange{99, (uint64_t)o, std::make_shared<int>(o)};
+      al.Hash(bad, origin);
+      parts_of.push_back(bad);
+    }
+    auto r = processor::ProcessHashActions(hasher, al);
+    EXPECT(r.ok(), "no error");
+    for (size_t i = 0; i < parts_of.size() && i < r.value.Len(); ++i)
+      EXPECT(r.value.Items()[i].digest == oracle(parts_of[i]), "storm digest == oracle");
+    uint32_t shards = 0;
+    uint64_t up = 0;
+    msha_shard_count(hasher.ctx(), &shards);
+    for (uint32_t k = 0; k < shards; ++k) {
+      msha_shard_stats st{};
+      msha_get_shard_stats(hasher.ctx(), k, &st);
+      up += st.h2d_payload_bytes;
+    }
+    EXPECT(up >= distinct - 16 * 2 * nodes && up <= distinct, "each distinct payload uploaded once");
+  }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;

@@ -65,7 +65,7 @@ def test_process_hash_actions_non_hash_action_error():
     from mirbft_amd.processor import Action
 
     class FakeHasher:
-        def hash_batch(self, parts):
+        def hash_requests(self, reqs):
             raise AssertionError("must fail before hashing")
 
     al = ActionList([Action(type="send")])
@@ -108,3 +108,29 @@ def test_checkpoint_hash_data_matches_streaming_active_hash():
         data = checkpoint_hash_data(prev, digests)
         assert hashlib.sha256(b"".join(data)).digest() == expect
         prev = expect
+
+
+def test_epoch_change_aliases_by_object_and_content():
+    """The packing rule the Go drop-in and the Python mirror share
+    (processor._epoch_change_aliases): the same EpochChange object, or an equal
+    payload from the same origin node, reuses the first request's payload; an
+    altered copy, another origin, or a non-EpochChange origin does not."""
+    from mirbft_amd.encoding import Checkpoint, EpochChange, SetEntry, epoch_change_hash_data
+    from mirbft_amd.processor import ActionHashRequest, HashOriginEpochChange, _epoch_change_aliases
+
+    def ec(seed):
+        return EpochChange(new_epoch=3, checkpoints=[Checkpoint(seq_no=20, value=bytes([seed]) * 40)],
+                           p_set=[SetEntry(epoch=2, seq_no=s, digest=bytes([s, seed]) * 16) for s in range(5)],
+                           q_set=[])
+
+    a, b = ec(1), ec(2)
+    a_copy, a_bad = ec(1), ec(1)
+    a_bad.p_set[0] = SetEntry(epoch=2, seq_no=0, digest=bytes([0xEE]) * 32)
+
+    def req(m, origin, src=0):
+        return ActionHashRequest(data=epoch_change_hash_data(m),
+                                 origin=HashOrigin(HashOriginEpochChange(source=src, origin=origin, epoch_change=m)))
+    reqs = [req(a, 0), req(a, 0, 1), req(b, 1), req(a_copy, 0, 2), req(a_bad, 0, 3), req(a_copy, 0, 4),
+            req(ec(1), 5), ActionHashRequest(data=epoch_change_hash_data(a), origin=HashOrigin(HashOriginBatch(0, 0, 1))),
+            req(b, 1, 9)]
+    assert _epoch_change_aliases(reqs) == [-1, 0, -1, 0, -1, 0, -1, -1, 2]

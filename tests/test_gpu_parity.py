@@ -1090,3 +1090,52 @@ def test_small_path_limits(engine, monkeypatch):
     st0 = engine.stats()["small_calls"]
     assert np.array_equal(engine.digest_batch(w.arena, w.off[:100], w.len[:100]), exp[:100])
     assert engine.stats()["small_calls"] == st0
+
+
+@pytest.mark.parametrize("nodes", [24, 100])
+def test_epoch_change_storm_packed_once(engine, nodes):
+    """An epoch-change storm through the Python mirror (epoch_target.go:486-528:
+    every origin's EpochChange hashed once per ack): acks sharing the
+    originator's object (the testengine), equal copies (off the wire) and one
+    altered copy per origin. Each distinct payload is packed and uploaded once
+    (h2d_payload_bytes = the packed span), every digest equals the oracle's.
+    24 nodes take the latency path (a pinned span), 100 the direct path."""
+    from mirbft_amd.encoding import Checkpoint, SetEntry, epoch_change_hash_data
+    rng = np.random.default_rng(nodes)
+    hasher = GPUHasher(engine)
+    al, want, total = ActionList(), [], 0
+    for o in range(nodes):
+        ec = EpochChange(new_epoch=9, checkpoints=[Checkpoint(seq_no=500 * (j + 1), value=rng.bytes(332))
+                                                   for j in range(2)],
+                         p_set=[SetEntry(epoch=8, seq_no=s, digest=rng.bytes(32))
+                                for s in range(int(rng.integers(0, 1000)))],
+                         q_set=[SetEntry(epoch=7, seq_no=s, digest=rng.bytes(32))
+                                for s in range(int(rng.integers(0, 300)))])
+        parts = epoch_change_hash_data(ec)
+        payload = b"".join(parts)
+        for src in range(nodes):
+            m = ec
+            if src % 3 == 1:   # an equal copy: another object, the same fields
+                m = EpochChange(new_epoch=ec.new_epoch, checkpoints=list(ec.checkpoints), p_set=list(ec.p_set),
+                                q_set=list(ec.q_set))
+            al.hash(parts if m is ec else epoch_change_hash_data(m),
+                    HashOrigin(HashOriginEpochChange(source=src, origin=o, epoch_change=m)))
+            want.append(hashlib.sha256(payload).digest() if src == 0 else want[-1])
+            total += len(payload)
+        bad = EpochChange(new_epoch=ec.new_epoch, checkpoints=[Checkpoint(seq_no=500, value=bytes(332)),
+                                                               ec.checkpoints[1]],
+                          p_set=list(ec.p_set), q_set=list(ec.q_set))
+        bad_parts = epoch_change_hash_data(bad)
+        al.hash(bad_parts, HashOrigin(HashOriginEpochChange(source=999, origin=o, epoch_change=bad)))
+        want.append(hashlib.sha256(b"".join(bad_parts)).digest())
+        total += len(payload)
+    events = ProcessHashActions(hasher, al)
+    assert [e.type.hash_result.digest for e in events] == want
+    pk = hasher.last_pack
+    assert pk["payloads"] == 2 * nodes and pk["aliased"] == nodes * nodes - nodes
+    up = sum(s["h2d_payload_bytes"] for s in engine.shard_stats())
+    assert pk["packed_bytes"] - 16 <= up <= pk["packed_bytes"], (up, pk)
+    assert up * (nodes // 2) < total      # vs packing every ack
+    st = engine.stats()
+    assert (st["small_calls"] > 0) if nodes == 24 else (st["direct_calls"] > 0)
+    hasher.close()
