@@ -99,7 +99,8 @@ typedef struct {
  * milliseconds since the call began. */
 typedef struct {
   int32_t device;              /* HIP device id */
-  uint32_t reserved;
+  uint32_t head_lanes;         /* pinned arenas: long chains run as heads (two-lane chain kernel, CUs of
+                                  their own, payloads uploaded first; ABI 8) */
   uint64_t messages;           /* messages of this shard */
   uint64_t lanes;              /* distinct payloads hashed (aliases fold) */
   uint64_t h2d_payload_bytes;  /* message bytes uploaded (compacted byte ranges or staged chunks) */

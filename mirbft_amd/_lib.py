@@ -61,7 +61,7 @@ class MshaStats(ctypes.Structure):
 class MshaShardStats(ctypes.Structure):
     _fields_ = [
         ("device", ctypes.c_int32),
-        ("reserved", ctypes.c_uint32),
+        ("head_lanes", ctypes.c_uint32),
         ("messages", ctypes.c_uint64),
         ("lanes", ctypes.c_uint64),
         ("h2d_payload_bytes", ctypes.c_uint64),

@@ -87,13 +87,18 @@ struct PlanArgs {
   uint64_t tmask = 0;
   uint32_t* slot;         // m: each message's table slot (with table)
   uint32_t* rep;          // out, m: the first message with the same (off, len)
-  uint64_t chunks = 1;    // upload pieces of the shard
-  uint64_t B = 1;         // block-count classes per piece (1: pieces only)
-  uint64_t bmax = 0;      // largest block count (key = piece * B + bmax - blocks)
+  uint64_t pieces = 1;    // upload pieces of the shard
+  // Lane groups: one per (region, piece), region 0 = long chains (blocks >=
+  // long_blocks; long_blocks 0: no such region), region 1 = the rest; group
+  // g = region * pieces + piece, chunks = the number of groups.
+  uint64_t long_blocks = 0;
+  uint64_t chunks = 1;
+  uint64_t B = 1;         // block-count classes per group (1: groups only)
+  uint64_t bmax = 0;      // largest block count (key = group * B + bmax - blocks)
   uint64_t nb = 1;        // chunks * B buckets
   uint32_t* cnt;          // nb zeroed counters -> bucket starts
-  uint32_t* gmin;         // chunks entries, 0xFFFFFFFF-filled: lowest lane index per piece
-  uint32_t* cut;          // out, chunks + 1: first lane of each piece's group
+  uint32_t* gmin;         // chunks entries, 0xFFFFFFFF-filled: lowest lane index per group
+  uint32_t* cut;          // out, chunks + 1: first lane of each group
   uint32_t* info;         // out: [0] = lanes
   uint64_t* lane_off;     // out, per lane: device offset, length, digest slot
   uint64_t* lane_len;

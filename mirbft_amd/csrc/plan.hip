@@ -154,14 +154,19 @@ __device__ __forceinline__ void wave_count(TileTable& t, uint32_t* gcnt, uint32_
   }
 }
 
-// Bucket key of message i when it is a lane (rep[i] == i): (piece holding the
-// payload's end) * B + (bmax - blocks).
+// Bucket key of message i when it is a lane (rep[i] == i): group * B + (bmax -
+// blocks), group = region * pieces + (piece holding the payload's end); region
+// 0 holds the long chains (the host uploads their payloads first and runs them
+// on a head kernel of their own), region 1 the rest.
 __device__ __forceinline__ uint32_t lane_key(const PlanArgs& a, uint64_t i, uint32_t* chunk_out) {
   const uint64_t l = a.len[i];
   const uint64_t end = a.dev_off[i] + (l ? l : 1) - 1;
-  const uint32_t chunk = (uint32_t)min((uint64_t)(end >> kDirectChunkShift), a.chunks - 1);
+  const uint64_t blocks = dev_blocks_for(l);
+  const uint64_t region = a.long_blocks && blocks < a.long_blocks ? 1 : 0;
+  const uint32_t chunk = (uint32_t)(region * (a.chunks - a.pieces) + min((uint64_t)(end >> kDirectChunkShift),
+                                                                        a.pieces - 1));
   if (chunk_out) *chunk_out = chunk;
-  return chunk * (uint32_t)a.B + (a.B > 1 ? (uint32_t)(a.bmax - dev_blocks_for(l)) : 0u);
+  return chunk * (uint32_t)a.B + (a.B > 1 ? (uint32_t)(a.bmax - blocks) : 0u);
 }
 
 __global__ __launch_bounds__(256) void k_plan_keys(PlanArgs a) {

@@ -149,7 +149,7 @@ class Engine:
         for i in range(n.value):
             s = L.MshaShardStats()
             self._check(self._lib.msha_get_shard_stats(self._ctx, i, ctypes.byref(s)))
-            out.append({name: getattr(s, name) for name, _ in L.MshaShardStats._fields_ if name != "reserved"})
+            out.append({name: getattr(s, name) for name, _ in L.MshaShardStats._fields_})
         return out
 
     # -- host-memory entry points -----------------------------------------

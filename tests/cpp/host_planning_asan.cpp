@@ -223,18 +223,22 @@ static void scan_cases(std::mt19937_64& rng) {
 // 64 MiB device piece, and lanes whose payload ends in piece c are complete once
 // the uploads that end at or below (c+1) * 64 MiB are.
 static void direct_upload_cases(std::mt19937_64& rng) {
-  for (int shape = 0; shape < 5; ++shape) {
-    const uint64_t n = shape == 4 ? 3 : 40000;
+  for (int shape = 0; shape < 12; ++shape) {
+    // shapes 6..11: shapes 0..5 with long chains marked (their granules go up first)
+    const uint64_t long_blocks = shape >= 6 ? 256 : 0;
+    const int sh_kind = shape % 6;
+    const uint64_t n = sh_kind == 4 ? 3 : 40000;
     std::vector<uint64_t> off(n), len(n);
     uint64_t pos = 0;
     for (uint64_t i = 0; i < n; ++i) {
-      len[i] = shape == 0 ? 512 : rng() % 5000;
-      if (shape == 1 && rng() % 7 == 0) len[i] = 0;
+      len[i] = sh_kind == 0 ? 512 : rng() % 5000;
+      if (sh_kind == 1 && rng() % 7 == 0) len[i] = 0;
+      if (sh_kind == 5 && rng() % 100 == 0) len[i] = 16000 + rng() % 90000;  // long chains, scattered
       off[i] = pos;
       pos += (len[i] + 15) & ~15ull;
-      if (shape == 3 && rng() % 100 == 0) pos += rng() % (3u << 20);  // gaps: untouched granules
+      if (sh_kind == 3 && rng() % 100 == 0) pos += rng() % (3u << 20);  // gaps: untouched granules
     }
-    if (shape == 2)  // an aliased pool at the start (c5 shape): 5% point back into it
+    if (sh_kind == 2)  // an aliased pool at the start (c5 shape): 5% point back into it
       for (uint64_t i = 0; i < n; ++i)
         if (rng() % 20 == 0) {
           off[i] = (rng() % 50) * 4096;
@@ -247,14 +251,15 @@ static void direct_upload_cases(std::mt19937_64& rng) {
     for (auto& b : host) b = (uint8_t)rng();
     BatchScan sc;
     scan_batch(host.data(), arena_len, off.data(), len.data(), n, sc);
-    unsigned gs = shape == 3 ? 12 : 16;  // small granules: many runs
+    unsigned gs = sh_kind == 3 ? 12 : 16;  // small granules: many runs
     const uint64_t glo = sc.lo & ~((1ull << gs) - 1);
     const uint64_t nG = ((sc.hi - glo) >> gs) + 1;
     // the shard: the second half of the batch (a sub-range like a real shard)
     const uint64_t a = n / 2, m = n - a;
     std::vector<uint64_t> h_off(m), h_len(m);
     std::vector<uint8_t> mark(nG, 0);
-    const ShardSpan sh = stage_and_mark(off.data() + a, len.data() + a, m, glo, gs, h_off.data(), h_len.data(), mark);
+    const ShardSpan sh =
+        stage_and_mark(off.data() + a, len.data() + a, m, glo, gs, h_off.data(), h_len.data(), mark, long_blocks);
     bool staged = true;
     for (uint64_t i = 0; i < m; ++i) staged &= h_off[i] == off[a + i] && h_len[i] == len[a + i];
     CHECK(staged, "direct shape %d: staged metadata differs", shape);
@@ -265,7 +270,7 @@ static void direct_upload_cases(std::mt19937_64& rng) {
     std::vector<uint8_t> dev(dev_bytes + 64, 0xEE);
     uint64_t last_end = 0;
     bool inside = true, ascending = true, in_piece = true;
-    for_each_upload(gmap.data(), ng, gbase, glo, gs, sh.lo, sh.hi, [&](uint64_t p, uint64_t d, uint64_t bytes) {
+    for_each_upload(gmap.data(), mark, ng, gbase, glo, gs, sh.lo, sh.hi, [&](uint64_t p, uint64_t d, uint64_t bytes) {
       inside &= bytes > 0 && p + bytes <= arena_len && d + bytes <= dev_bytes;
       ascending &= d >= last_end;
       in_piece &= d / kDirectChunk == (d + bytes - 1) / kDirectChunk;
@@ -285,9 +290,23 @@ static void direct_upload_cases(std::mt19937_64& rng) {
     }
     CHECK(bad == 0, "direct shape %d: %llu messages not intact at their device offset", shape,
           (unsigned long long)bad);
-    if (shape == 2) {  // the pool's granules are uploaded, the first half's own bytes are not
+    if (long_blocks) {  // every long payload lies in the device prefix the long granules fill
+      uint64_t long_bytes = 0, late = 0, longs = 0;
+      for (uint64_t g = 0; g < ng; ++g) long_bytes += (mark[gbase + g] & kMarkLong) ? G : 0;
+      for (uint64_t i = 0; i < m; ++i) {
+        const uint64_t o = h_off[i], l = h_len[i];
+        if (!l || blocks_for(l) < long_blocks) continue;
+        ++longs;
+        const uint64_t r = o - glo;
+        late += gmap[(r >> gs) - gbase] + (r & (G - 1)) + l > long_bytes;
+      }
+      CHECK(late == 0 && (sh_kind != 5 || longs > 0), "direct shape %d: %llu of %llu long payloads not first",
+            shape, (unsigned long long)late, (unsigned long long)longs);
+    }
+    if (sh_kind == 2) {  // the pool's granules are uploaded, the first half's own bytes are not
       uint64_t total = 0;
-      for_each_upload(gmap.data(), ng, gbase, glo, gs, sh.lo, sh.hi, [&](uint64_t, uint64_t, uint64_t b) { total += b; });
+      for_each_upload(gmap.data(), mark, ng, gbase, glo, gs, sh.lo, sh.hi,
+                      [&](uint64_t, uint64_t, uint64_t b) { total += b; });
       CHECK(total < arena_len * 3 / 4, "direct shape 2: %llu of %llu bytes uploaded for half the batch",
             (unsigned long long)total, (unsigned long long)arena_len);
     }
