@@ -97,10 +97,15 @@ def parse():
                         "one libmirsha context over N GPUs (device_mask) and the host entry point "
                         "msha_digest_batch on a pinned arena (end-to-end, PCIe-inclusive)")
     p.add_argument("--pageable", action="store_true", help="with --mode lib: a pageable numpy arena")
+    p.add_argument("--unaliased", action="store_true",
+                   help="with --mode lib --config c5: every action packs its own copy of its payload, in "
+                        "action order (a caller that does not share EpochChange payloads between actions)")
     p.add_argument("--no-extra", action="store_true",
                    help="skip the extra_configs legs (one GPU: c3, c4, c5; N GPUs: c5 over all ranks)")
     p.add_argument("--no-host-api", action="store_true",
-                   help="skip the host_api leg (c5 through msha_digest_batch over all N GPUs, one process)")
+                   help="skip the host_api legs (c5 through msha_digest_batch over all N GPUs, one process)")
+    p.add_argument("--no-host-api-unaliased", action="store_true",
+                   help="skip host_api_unaliased (c5 with every action its own payload copy: ~24 GB pinned)")
     return p.parse_args()
 
 
@@ -257,7 +262,7 @@ def launch_ranks(args) -> int:
     return subprocess.run(cmd).returncode
 
 
-def host_api_leg(args, world: int) -> dict:
+def host_api_leg(args, world: int, unaliased: bool = False) -> dict:
     """The north-star host path over the job's N GPUs, reported beside the
     headline: ONE process, one libmirsha context over device_mask (1 << N) - 1,
     c5's 2^23 mixed actions (strong scaling: the node's storm split over its
@@ -274,23 +279,30 @@ def host_api_leg(args, world: int) -> dict:
         env["MSHA_VIRTUAL_SHARDS"] = str(world)
         gpus = 1
     cmd = [sys.executable, os.path.abspath(__file__), "--mode", "lib", "--config", "c5", "--gpus", str(gpus),
-           "--steps", "5", "--warmup", "2"]
+           "--steps", "3" if unaliased else "5", "--warmup", "1" if unaliased else "2"]
+    if unaliased:
+        cmd.append("--unaliased")
     try:
-        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
         lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
         if r.returncode != 0 or not lines:
             return {"error": f"rc={r.returncode}", "stderr_tail": r.stderr[-400:]}
         d = json.loads(lines[-1])
     except Exception as e:  # noqa: BLE001 -- reported, never fatal to the headline
         return {"error": repr(e)[:400]}
-    return {"what": "c5 2^23 mixed actions, pinned arena -> msha_digest_batch -> pinned digests, one process, "
-                    "one context over all the job's GPUs (PCIe-inclusive; NOT the headline)",
+    what = ("c5 2^23 mixed actions, pinned arena -> msha_digest_batch -> pinned digests, one process, "
+            "one context over all the job's GPUs (PCIe-inclusive; NOT the headline); ")
+    what += ("every action packs its own copy of its payload, in action order: 20+ GB of EpochChange "
+             "re-hashes cross PCIe (a caller that does not share payloads)" if unaliased else
+             "each distinct EpochChange payload packed once and named by every action that carries it "
+             "(what the Go drop-in packs since round 4: epochChangeAliases)")
+    return {"what": what, "arena_bytes": d["arena_bytes"],
             "value": d["value"], "unit": "digests/s", "n_gpus": d["n_gpus"], "shards": d["shards"],
             "virtual_shards": d["virtual_shards"], "ms_per_call": d["ms_per_step"], "call_ms": d["call_ms"],
             "gbps_hashed": d["gbps_hashed"], "steps": d["steps"], "plan_ms": d["last_call_stats"]["plan_ms"],
             "first_launch_ms_max": max(x["first_launch_ms"] for x in d["last_call_shards"]),
-            "per_gpu": [{k: x[k] for k in ("device", "messages", "lanes", "h2d_bytes", "device_ms", "upload_ms",
-                                           "kernel_ms", "first_launch_ms", "plan_kernel_ms")}
+            "per_gpu": [{k: x[k] for k in ("device", "messages", "lanes", "head_lanes", "h2d_bytes", "device_ms",
+                                           "upload_ms", "kernel_ms", "first_launch_ms", "plan_kernel_ms")}
                         for x in d["last_call_shards"]]}
 
 
@@ -513,6 +525,15 @@ def run_lib(args):
         w = {"c2": W.c2_requests, "c3": W.c3_batches, "c4": W.c4_large}[args.config](n=base * shards)
     arena, off, ln = w.arena, w.off, w.len
     out = np.empty((w.n, 32), dtype=np.uint8)
+    if args.unaliased:
+        # every action its own copy of its payload, packed in action order, pinned
+        from mirbft_amd import workloads as W
+        new_off, total = W.unaliased_layout(w)
+        pa = eng.pinned_empty(total + 64)
+        pa[total:] = 0
+        W.fill_unaliased(w, new_off, pa)
+        w = W.Workload(w.name + ", unaliased (each action its own payload copy, action order)", pa, new_off, w.len)
+        arena, off, ln = pa, None, None
     if not args.pageable:
         # what the cgo adapter does: payloads, off/len and the digests all in
         # msha_pinned_alloc memory, so every transfer is a DMA of the caller's bytes
@@ -520,7 +541,8 @@ def run_lib(args):
             p = eng.pinned_empty(a.nbytes).view(a.dtype).reshape(a.shape)
             p[...] = a
             return p
-        arena, off, ln = pinned(w.arena), pinned(w.off), pinned(w.len)
+        arena = w.arena if args.unaliased else pinned(w.arena)
+        off, ln = pinned(w.off), pinned(w.len)
         out = eng.pinned_empty(w.n * 32).reshape(w.n, 32)
     for _ in range(max(1, args.warmup)):
         eng.digest_batch(arena, off, ln, out=out)
@@ -537,6 +559,7 @@ def run_lib(args):
     print(json.dumps({
         "metric": "end-to-end host API msha_digest_batch (pack + H2D + kernel + D2H), NOT the headline",
         "mode": "lib", "arena": "pageable numpy" if args.pageable else "pinned (msha_pinned_alloc), off/len pinned",
+        "unaliased": bool(args.unaliased), "arena_bytes": int(w.arena.size),
         "value": w.n * args.steps / el, "unit": "digests/s", "n_gpus": n_gpus, "shards": shards,
         "virtual_shards": os.environ.get("MSHA_VIRTUAL_SHARDS"),
         "gbps_hashed": w.message_bytes * args.steps / el / 1e9, "steps": args.steps,
@@ -666,6 +689,8 @@ def main():
             line["cpu_baseline"] = cpu_baseline(w, args.cpu_seconds)
         if not args.no_host_api:
             line["host_api"] = host_api_leg(args, world)
+            if not args.no_host_api_unaliased:
+                line["host_api_unaliased"] = host_api_leg(args, world, unaliased=True)
         print(json.dumps(line), flush=True)
 
 

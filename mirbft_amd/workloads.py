@@ -77,6 +77,7 @@ class Workload:
     idx: Optional[np.ndarray] = None
     begin: Optional[np.ndarray] = None
     uniform_stride: Optional[int] = None   # set when message i starts at i*stride
+    shared: Optional[np.ndarray] = None    # c5: True where the message names a shared (aliased) payload
 
     @property
     def n(self) -> int:
@@ -179,4 +180,49 @@ def c5_storm(n: int = 1 << 23, first: int = 0, pool: Optional[list] = None) -> W
         arena[int(o): int(o) + len(p)] = np.frombuffer(p, dtype=np.uint8)
     arena[pool_bytes: pool_bytes + own_total] = random_bytes(SEED ^ 0x55, 0, own_total)
     off = np.where(own, own_off + np.uint64(pool_bytes), pool_off[ec_pick]).astype(np.uint64)
-    return Workload(f"c5: {n} mixed actions (70/25/5)", arena, off, length)
+    return Workload(f"c5: {n} mixed actions (70/25/5)", arena, off, length, shared=~own)
+
+
+def unaliased_layout(w: Workload):
+    """w's messages packed the way a caller without payload sharing packs an
+    ActionList (every action its own copy, in action order, 16-byte aligned:
+    go/pkg/processor/gpuhash.go before round 4's epochChangeAliases): (offsets,
+    arena bytes)."""
+    steps = (w.len + np.uint64(15)) // np.uint64(16) * np.uint64(16)
+    off = np.zeros(w.n, dtype=np.uint64)
+    if w.n > 1:
+        off[1:] = np.cumsum(steps)[:-1]
+    return off, int(steps.sum())
+
+
+def fill_unaliased(w: Workload, new_off: np.ndarray, dst: np.ndarray, threads: int = 16) -> None:
+    """Copy w's payloads into dst at new_off (unaliased_layout). Messages that own
+    their payload are contiguous runs in both layouts (copied run by run); every
+    shared-payload message gets its own copy."""
+    assert w.shared is not None
+    sh = np.flatnonzero(w.shared)
+    # runs of own messages between shared ones: [a, b)
+    starts = np.concatenate([[0], sh + 1])
+    ends = np.concatenate([sh, [w.n]])
+    keep = ends > starts
+    runs = list(zip(starts[keep].tolist(), ends[keep].tolist()))
+
+    def copy_part(part):
+        lo, hi = part
+        for a, b in runs[lo:hi]:
+            src0 = int(w.off[a])
+            nb = int(w.off[b - 1]) + int(w.len[b - 1]) - src0
+            d0 = int(new_off[a])
+            dst[d0:d0 + nb] = w.arena[src0:src0 + nb]
+
+    def copy_shared(part):
+        lo, hi = part
+        for i in sh[lo:hi].tolist():
+            o, l, d0 = int(w.off[i]), int(w.len[i]), int(new_off[i])
+            dst[d0:d0 + l] = w.arena[o:o + l]
+
+    from concurrent.futures import ThreadPoolExecutor
+    T = max(1, threads)
+    with ThreadPoolExecutor(max_workers=T) as ex:
+        list(ex.map(copy_part, [(len(runs) * t // T, len(runs) * (t + 1) // T) for t in range(T)]))
+        list(ex.map(copy_shared, [(len(sh) * t // T, len(sh) * (t + 1) // T) for t in range(T)]))
