@@ -723,6 +723,8 @@ constexpr int kCoopSlotQuads = 16;
 #define MSHA_C8(q)                                                     \
   {                                                                    \
     const uint4 v0 = kv[q], v1 = kv[(q) + 1];                          \
+    nxt[q] = nslot[(q) * 64];                                          \
+    nxt[(q) + 1] = nslot[((q) + 1) * 64];                              \
     MSHA_CROUND(a, b, c, d, e, f, g, h, v0.x)                          \
     MSHA_CROUND(h, a, b, c, d, e, f, g, v0.y)                          \
     MSHA_CROUND(g, h, a, b, c, d, e, f, v0.z)                          \
@@ -733,13 +735,12 @@ constexpr int kCoopSlotQuads = 16;
     MSHA_CROUND(b, c, d, e, f, g, h, a, v1.w)                          \
   }
 
-// Consumer: the 64 rounds of one block from a K+W slot (lane's column).
-__device__ __forceinline__ void compress_kw(State& s, const uint4* __restrict__ slot) {
-  // All 16 reads issued up front (64 VGPRs; this kernel runs at low
-  // occupancy): one LDS latency per block instead of one per quad.
-  uint4 kv[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) kv[q] = slot[q * 64];
+// Consumer: the 64 rounds of one block from its K+W quads kv (read from LDS
+// during the previous block), reading the next block's quads from nslot (the
+// lane's column of the other slot) into nxt meanwhile, so no block waits for
+// an LDS round trip (k_digest_coop alternates the two register sets).
+__device__ __forceinline__ void compress_kw(State& s, const uint4 (&kv)[16], uint4 (&nxt)[16],
+                                            const uint4* __restrict__ nslot) {
   uint32_t a = s.h[0], b = s.h[1], c = s.h[2], d = s.h[3];
   uint32_t e = s.h[4], f = s.h[5], g = s.h[6], h = s.h[7];
   MSHA_C8(0) MSHA_C8(2) MSHA_C8(4) MSHA_C8(6) MSHA_C8(8) MSHA_C8(10) MSHA_C8(12) MSHA_C8(14)
@@ -845,14 +846,27 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
       }
       if (active && b + 1 <= nfull) load_block16<MODE>(p + 64 * (uint64_t)(b + 1), raw);  // prefetch
       schedule_kw(w, &kw[b & 1][group][lane]);
-      __syncthreads();
+      __syncthreads();  // barrier b: slot b & 1 holds block b
     }
+    __syncthreads();  // barrier NB: the consumers' last (they wait one block ahead)
   } else {
+    // As in k_digest_chain2: block b's K+W is read during block b-1 (barrier
+    // b+1 opens block b once slot (b+1) & 1 is written; the producer refills
+    // the slot block b-1 read, complete at barrier b+1), two register sets
+    // alternating by unrolling the block loop twice.
     State s;
     state_init(s);
+    uint4 ka[16], kb[16];
+    __syncthreads();  // barrier 0
+#pragma unroll
+    for (int q = 0; q < 16; ++q) ka[q] = kw[0][group][q * 64 + lane];
     for (uint32_t b = 0; b < NB; ++b) {
-      __syncthreads();
-      compress_kw(s, &kw[b & 1][group][lane]);
+      __syncthreads();  // barrier b+1
+      compress_kw(s, ka, kb, &kw[(b + 1) & 1][group][lane]);  // a read past the last block is unused
+      if (active && b + 1 == nb) store_digest(s, out + 32 * o);
+      if (++b == NB) break;
+      __syncthreads();  // barrier b+1
+      compress_kw(s, kb, ka, &kw[(b + 1) & 1][group][lane]);
       if (active && b + 1 == nb) store_digest(s, out + 32 * o);
     }
   }
