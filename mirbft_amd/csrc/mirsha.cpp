@@ -1594,6 +1594,9 @@ void run_pipeline(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* len, con
 // (so one at the arena's very end uploads nothing past it).
 struct ShardSpan {
   uint64_t lo = UINT64_MAX, hi = 0, sum = 0, g0 = UINT64_MAX, g1 = 0;
+  // some message starts at or below an earlier message's start (the candidates-
+  // first test of alias_uids): only then can two messages share (off, len)
+  bool backward = false;
   bool any() const { return hi > 0; }
 };
 
@@ -1610,15 +1613,21 @@ ShardSpan stage_and_mark_t(const uint64_t* O, const uint64_t* L, uint64_t m, uin
                            uint64_t* h_off, uint64_t* h_len, std::vector<uint8_t>& mark, uint64_t long_blocks) {
   const unsigned T = plan_threads(m);
   std::vector<ShardSpan> acc(T);
+  std::vector<uint64_t> omin(T, UINT64_MAX), omax(T, 0);
   parallel_chunks(m, T, [&](unsigned t, uint64_t a, uint64_t b) {
     uint64_t lo = UINT64_MAX, hi = 0, sum = 0;
     uint64_t last = UINT64_MAX;  // the granule this thread marked last
+    uint64_t first_off = UINT64_MAX, max_off = 0;
+    bool backward = false;
     for (uint64_t i = a; i < b; ++i) {
       const uint64_t o = O[i], l = L[i];
       if (kStage) {
         h_off[i] = o;
         h_len[i] = l;
       }
+      backward |= i > a && o <= max_off;
+      max_off = i > a ? std::max(max_off, o) : o;
+      if (i == a) first_off = o;
       if (!l) continue;
       const uint64_t e = o + l;
       lo = std::min(lo, o);
@@ -1644,12 +1653,22 @@ ShardSpan stage_and_mark_t(const uint64_t* O, const uint64_t* L, uint64_t m, uin
     r.lo = lo;
     r.hi = hi;
     r.sum = sum;
+    r.backward = backward;
+    omin[t] = first_off;  // the chunk's first start: compared with the earlier chunks' largest
+    omax[t] = max_off;
   });
   ShardSpan sh;
-  for (const ShardSpan& r : acc) {
+  uint64_t run = 0;
+  bool seen = false;
+  for (unsigned t = 0; t < T; ++t) {
+    const ShardSpan& r = acc[t];
     sh.lo = std::min(sh.lo, r.lo);
     sh.hi = std::max(sh.hi, r.hi);
     sh.sum += r.sum;
+    if (omin[t] == UINT64_MAX && omax[t] == 0) continue;  // an empty chunk
+    sh.backward |= r.backward || (seen && omin[t] <= run);
+    run = seen ? std::max(run, omax[t]) : omax[t];
+    seen = true;
   }
   if (sh.any()) {  // the granules of the span's ends are the extreme marked ones
     sh.g0 = (sh.lo - glo) >> gs;
@@ -1985,7 +2004,10 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
     // with streams of several shards sharing a GPU's hardware queues (HIP
     // multiplexes streams over GPU_MAX_HW_QUEUES), a planner queued behind
     // another stream's payload or kernel waits would wait for them too.
-    const bool aliases = m > 1 && any && sh.sum > sh.hi - sh.lo;  // overlapping payloads: maybe aliases
+    // a message at or below an earlier start may repeat a payload: fold aliases
+    // (a span test -- bytes > span -- missed a shard whose own messages are sparse
+    // in the arena while its EpochChange re-hashes point back into a shared pool)
+    const bool aliases = m > 1 && any && sh.backward;
     const uint64_t B = chunks * (sc.bmax + 1) <= (1u << 20) ? sc.bmax + 1 : 1;
     const uint64_t nb = chunks * B;
     uint64_t cap = 1024;

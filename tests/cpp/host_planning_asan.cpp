@@ -264,6 +264,17 @@ static void direct_upload_cases(std::mt19937_64& rng) {
     for (uint64_t i = 0; i < m; ++i) staged &= h_off[i] == off[a + i] && h_len[i] == len[a + i];
     CHECK(staged, "direct shape %d: staged metadata differs", shape);
     CHECK(sh.any(), "direct shape %d: no payload", shape);
+    {  // backward: some message starts at or below an earlier one (may alias)
+      bool back = false;
+      uint64_t mx = 0;
+      for (uint64_t i = 0; i < m; ++i) {
+        back |= i > 0 && off[a + i] <= mx;
+        mx = i ? std::max(mx, off[a + i]) : off[a + i];
+      }
+      CHECK(sh.backward == back, "direct shape %d: backward %d, want %d", shape, (int)sh.backward, (int)back);
+      CHECK(sh_kind != 2 || back, "direct shape %d: the aliased pool is not seen", shape);
+      CHECK(sh_kind != 0 || !back, "direct shape %d: a forward batch flagged", shape);
+    }
     const uint64_t gbase = sh.g0, ng = sh.g1 - sh.g0 + 1;
     std::vector<uint64_t> gmap(ng);
     const uint64_t dev_bytes = build_gmap(mark, gbase, ng, gs, gmap.data());
