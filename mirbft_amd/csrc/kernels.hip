@@ -888,35 +888,49 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
 // producer wave (64 messages: loads, padding, K+W schedules into LDS, as in
 // k_digest_coop) and two consumer waves of 32 messages; EXCL as above (the
 // head's CUs hold nothing else); each lane stores its side's four digest words.
-// Both DPP adds sit in ONE asm statement with an s_nop 0 between them: a DPP
-// read of a VGPR needs 2 wait states after the VALU write of it, the compiler's
-// hazard recognizer does not look inside asm text, and u_ (read through DPP by
-// the second add) may be written by the instruction right before the first.
-// The first add's DPP source (W) was written four rounds earlier.
-// tools/check_dpp_hazards.py checks every DPP of the built library for it.
+// The rounds are inline asm (MSHA_D4 below): a DPP read of a VGPR needs 2 wait
+// states after the VALU write of it, and the compiler's hazard recognizer does
+// not look inside asm text, so the asm orders its own instructions to satisfy
+// that, and tools/check_dpp_hazards.py checks every DPP of the built library.
 // ---------------------------------------------------------------------------
-#define MSHA_DROUND(X, Y, Z, W, kw)                                                              \
-  {                                                                                              \
-    const uint32_t s_ = xor3(__builtin_amdgcn_alignbit(X, X, sh1), __builtin_amdgcn_alignbit(X, X, sh2), \
-                             __builtin_amdgcn_alignbit(X, X, sh3));                              \
-    const uint32_t u_ = s_ + ch(X, Y, Z) + (W + (kw));                                           \
-    uint32_t t_ = s_ + maj(X, Y, Z) + (kw);                                                      \
-    asm volatile("v_add_u32_dpp %0, %1, %2 row_mirror row_mask:0xf bank_mask:0x3\n\t"            \
-                 "s_nop 0\n\t"                                                                   \
-                 "v_add_u32_dpp %0, %2, %0 row_mirror row_mask:0xf bank_mask:0xc"                \
-                 : "+v"(t_) : "v"(W), "v"(u_));                                                  \
-    W = t_;                                                                                      \
-  }
+// One round in asm (X Y Z W: this lane's side, newest to oldest; the new word
+// replaces W). Named operands: sh1-3 the lane's rotate amounts, k the lane's
+// K+W word (0 in a-lanes), s1 s2 s3 s sk c u m t scratch.
+#define MSHA_ASM_ROUND(X, Y, Z, W, K)                                                            \
+  "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh1]\n\t"                                       \
+  "v_alignbit_b32 %[s2], %[" #X "], %[" #X "], %[sh2]\n\t"                                       \
+  "v_alignbit_b32 %[s3], %[" #X "], %[" #X "], %[sh3]\n\t"                                       \
+  "v_bitop3_b32 %[s], %[s1], %[s2], %[s3] bitop3:0x96\n\t"                                      \
+  "v_add_u32 %[sk], %[s], %[" #K "]\n\t"                                                          \
+  "v_bitop3_b32 %[c], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xca\n\t"                           \
+  "v_add3_u32 %[u], %[sk], %[" #W "], %[c]\n\t"                                                   \
+  "v_bitop3_b32 %[m], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xe8\n\t"                           \
+  "v_add_u32 %[t], %[sk], %[m]\n\t"                                                               \
+  "v_add_u32_dpp %[" #W "], %[" #W "], %[u] row_mirror row_mask:0xf bank_mask:0x3\n\t"           \
+  "v_add_u32_dpp %[" #W "], %[u], %[t] row_mirror row_mask:0xf bank_mask:0xc\n\t"
 // Four rounds from quad q of cur; the same quad of the NEXT block is read from
-// LDS slot nxt meanwhile, so its latency hides under the rounds.
-#define MSHA_D4(cur, nxt, q)                       \
-  {                                                \
-    const uint4 v_ = cur[q];                       \
-    nxt[q] = kw[ns][col + (q) * qstride];          \
-    MSHA_DROUND(X, Y, Z, W, v_.x)                  \
-    MSHA_DROUND(W, X, Y, Z, v_.y)                  \
-    MSHA_DROUND(Z, W, X, Y, v_.z)                  \
-    MSHA_DROUND(Y, Z, W, X, v_.w)                  \
+// LDS slot nxt meanwhile, so its latency hides under the rounds. The four
+// rounds are ONE asm statement: a lone wave issues one instruction per ~4.6
+// cycles whatever it is, and the compiler puts an s_nop after every asm
+// statement whose output the next VALU instruction reads (it cannot see
+// whether the asm ended in a dst-forwarding instruction) -- with a statement
+// per round that was 2 s_nops a round, 13 issue slots instead of 11 (+16 % a
+// block; tools/chain2_anatomy.hip). Inside, every DPP read is hazard-free by
+// construction: a round's second DPP reads u three instructions after writing
+// it (m, t and the first DPP between), and its first DPP reads W, written four
+// rounds earlier (tools/check_dpp_hazards.py checks the built library).
+#define MSHA_D4(cur, nxt, q)                                                                     \
+  {                                                                                              \
+    const uint4 v_ = cur[q];                                                                     \
+    nxt[q] = kw[ns][col + (q) * qstride];                                                        \
+    uint32_t s1_, s2_, s3_, s_, sk_, c_, u_, m_, t_;                                             \
+    asm volatile(MSHA_ASM_ROUND(X, Y, Z, W, k0) MSHA_ASM_ROUND(W, X, Y, Z, k1)                   \
+                 MSHA_ASM_ROUND(Z, W, X, Y, k2) MSHA_ASM_ROUND(Y, Z, W, X, k3)                   \
+                 : [X] "+v"(X), [Y] "+v"(Y), [Z] "+v"(Z), [W] "+v"(W), [s1] "=&v"(s1_),          \
+                   [s2] "=&v"(s2_), [s3] "=&v"(s3_), [s] "=&v"(s_), [sk] "=&v"(sk_), [c] "=&v"(c_), \
+                   [u] "=&v"(u_), [m] "=&v"(m_), [t] "=&v"(t_)                                   \
+                 : [sh1] "v"(sh1), [sh2] "v"(sh2), [sh3] "v"(sh3), [k0] "v"(v_.x), [k1] "v"(v_.y), \
+                   [k2] "v"(v_.z), [k3] "v"(v_.w));                                              \
   }
 // One block b from cur (read during the previous block), reading block b+1's
 // K+W (slot ns) into nxt; the digest is stored after the message's last block.
@@ -932,6 +946,25 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
       *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =                                     \
           make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));                                      \
   }
+
+// Diagnostic build only (tools/chain2_anatomy.hip defines MSHA_CHAIN2_STAMPS):
+// lane 0 of each wave of workgroup 0 stamps s_memtime before and after every
+// barrier, stamps[wave * 4096 + 2 j (+1)] for barrier j. The product build has
+// no stamps.
+#ifdef MSHA_CHAIN2_STAMPS
+__device__ uint64_t* g_chain2_stamps;
+#define MSHA_C2_BARRIER(j)                                                                      \
+  {                                                                                             \
+    const uint64_t j_ = (j);                                                                    \
+    if (blockIdx.x == 0 && lane == 0 && j_ < 2047)                                              \
+      g_chain2_stamps[wave * 4096 + 2 * j_] = __builtin_amdgcn_s_memtime();                     \
+    __syncthreads();                                                                            \
+    if (blockIdx.x == 0 && lane == 0 && j_ < 2047)                                              \
+      g_chain2_stamps[wave * 4096 + 2 * j_ + 1] = __builtin_amdgcn_s_memtime();                 \
+  }
+#else
+#define MSHA_C2_BARRIER(j) __syncthreads();
+#endif
 
 // Also AUTO's kernel for launches of at most 64 messages per CU (a call of a
 // few actions at low load: one chain's latency is the call's), where every
@@ -1004,9 +1037,9 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
       }
       if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
       schedule_kw(w, &kw[b & 1][lane]);
-      __syncthreads();  // barrier b: slot b & 1 holds block b
+      MSHA_C2_BARRIER(b)  // barrier b: slot b & 1 holds block b
     }
-    __syncthreads();  // barrier NB: the consumers' last (they wait one block ahead)
+    MSHA_C2_BARRIER(NB)  // barrier NB: the consumers' last (they wait one block ahead)
   } else {
     // e-side: e f g h, rotates 6 11 25; a-side: a b c d, rotates 2 13 22
     uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
@@ -1022,15 +1055,15 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     // register sets alternate by unrolling the block loop twice, so nothing is
     // copied between blocks.
     uint4 ka[16], kb[16];
-    __syncthreads();  // barrier 0: slot 0 holds block 0
+    MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds block 0
 #pragma unroll
     for (int q = 0; q < 16; ++q) ka[q] = kw[0][col + q * qstride];
     for (uint32_t b = 0; b < NB; ++b) {
-      __syncthreads();  // barrier b+1
+      MSHA_C2_BARRIER(b + 1)
       unsigned ns = (b + 1) & 1;  // a read past the last block is harmless (unused)
       MSHA_DBLOCK(ka, kb)
       if (++b == NB) break;
-      __syncthreads();  // barrier b+1
+      MSHA_C2_BARRIER(b + 1)
       ns = (b + 1) & 1;
       MSHA_DBLOCK(kb, ka)
     }
@@ -1038,7 +1071,8 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
 }
 #undef MSHA_DBLOCK
 #undef MSHA_D4
-#undef MSHA_DROUND
+#undef MSHA_ASM_ROUND
+#undef MSHA_C2_BARRIER
 
 // Uniform layout: message i is arena[i*stride : i*stride + msg_len].
 template <int MODE>
