@@ -919,9 +919,10 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
 // construction: a round's second DPP reads u three instructions after writing
 // it (m, t and the first DPP between), and its first DPP reads W, written four
 // rounds earlier (tools/check_dpp_hazards.py checks the built library).
-#define MSHA_D4(cur, q)                                                                          \
+#define MSHA_D4(cur, nxt, q)                                                                     \
   {                                                                                              \
     const uint4 v_ = cur[q];                                                                     \
+    nxt[q] = kw[ns][col + (q) * qstride];                                                        \
     uint32_t s1_, s2_, s3_, s_, sk_, c_, u_, m_, t_;                                             \
     asm volatile(MSHA_ASM_ROUND(X, Y, Z, W, k0) MSHA_ASM_ROUND(W, X, Y, Z, k1)                   \
                  MSHA_ASM_ROUND(Z, W, X, Y, k2) MSHA_ASM_ROUND(Y, Z, W, X, k3)                   \
@@ -929,67 +930,41 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
                    [s2] "=&v"(s2_), [s3] "=&v"(s3_), [s] "=&v"(s_), [sk] "=&v"(sk_), [c] "=&v"(c_), \
                    [u] "=&v"(u_), [m] "=&v"(m_), [t] "=&v"(t_)                                   \
                  : [sh1] "v"(sh1), [sh2] "v"(sh2), [sh3] "v"(sh3), [k0] "v"(v_.x), [k1] "v"(v_.y), \
-                   [k2] "v"(v_.z), [k3] "v"(v_.w)                                                \
-                 : "memory");                                                                    \
+                   [k2] "v"(v_.z), [k3] "v"(v_.w));                                              \
   }
-// Quad q of the next block's K+W into nxt (issued between the asm statements,
-// whose "memory" clobber keeps the reads where they are written).
-#define MSHA_PF(nxt, q) nxt[q] = kw[ns][col + (q) * qstride];
 // One block b from cur (read during the previous block), reading block b+1's
-// K+W (slot ns) into nxt once the producer has published it (s_ready > b + 1;
-// the poll's load is issued before the first four rounds, so its latency hides
-// under them); then, the reads complete, this consumer marks the slot read
-// (s_done). The digest is stored after the message's last block.
+// K+W (slot ns) into nxt; the digest is stored after the message's last block.
 #define MSHA_DBLOCK(cur, nxt)                                                                          \
   {                                                                                                    \
-    const unsigned ns = (b + 1) % kC2Slots;                                                            \
-    uint32_t ready = __hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);      \
     uint32_t X = H0, Y = H1, Z = H2, W = H3;                                                           \
-    MSHA_D4(cur, 0)                                                                                    \
-    MSHA_C2_STAMP(2 * (b + 1))                                                                         \
-    if (b + 1 < NB)                                                                                    \
-      while (ready < b + 2) /* no sleep: the consumers' wait is the chain's */                        \
-        ready = __hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);            \
-    MSHA_C2_STAMP(2 * (b + 1) + 1)                                                                     \
-    MSHA_PF(nxt, 0) MSHA_D4(cur, 1) MSHA_PF(nxt, 1) MSHA_D4(cur, 2) MSHA_PF(nxt, 2) MSHA_D4(cur, 3)    \
-    MSHA_PF(nxt, 3) MSHA_D4(cur, 4) MSHA_PF(nxt, 4) MSHA_D4(cur, 5) MSHA_PF(nxt, 5) MSHA_D4(cur, 6)    \
-    MSHA_PF(nxt, 6) MSHA_D4(cur, 7) MSHA_PF(nxt, 7) MSHA_D4(cur, 8) MSHA_PF(nxt, 8) MSHA_D4(cur, 9)    \
-    MSHA_PF(nxt, 9) MSHA_D4(cur, 10) MSHA_PF(nxt, 10) MSHA_D4(cur, 11) MSHA_PF(nxt, 11)                \
-    MSHA_D4(cur, 12) MSHA_PF(nxt, 12) MSHA_D4(cur, 13) MSHA_PF(nxt, 13) MSHA_D4(cur, 14)               \
-    MSHA_PF(nxt, 14) MSHA_PF(nxt, 15) MSHA_D4(cur, 15)                                                 \
+    MSHA_D4(cur, nxt, 0) MSHA_D4(cur, nxt, 1) MSHA_D4(cur, nxt, 2) MSHA_D4(cur, nxt, 3)              \
+    MSHA_D4(cur, nxt, 4) MSHA_D4(cur, nxt, 5) MSHA_D4(cur, nxt, 6) MSHA_D4(cur, nxt, 7)              \
+    MSHA_D4(cur, nxt, 8) MSHA_D4(cur, nxt, 9) MSHA_D4(cur, nxt, 10) MSHA_D4(cur, nxt, 11)            \
+    MSHA_D4(cur, nxt, 12) MSHA_D4(cur, nxt, 13) MSHA_D4(cur, nxt, 14) MSHA_D4(cur, nxt, 15)          \
     H0 += X; H1 += Y; H2 += Z; H3 += W;                                                                \
     if (active && b + 1 == nb)                                                                         \
       *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =                                     \
           make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));                                      \
-    /* release: the reads of slot ns are complete (lgkmcnt) before the mark */                        \
-    if (lane == 0) __hip_atomic_store(&s_done[wave - 1], b + 2, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP); \
   }
 
 // Diagnostic build only (tools/chain2_anatomy.hip defines MSHA_CHAIN2_STAMPS):
-// lane 0 of each wave of workgroup 0 stamps s_memtime around every wait for the
-// other side (consumers: before / after waiting for block b+1's K+W at stamps
-// 2 (b+1) and 2 (b+1) + 1; producer: before / after waiting for slot b to be
-// free at 2 b and 2 b + 1), stamps[wave * 4096 + k]. The product build has no
-// stamps.
+// lane 0 of each wave of workgroup 0 stamps s_memtime before and after every
+// barrier, stamps[wave * 4096 + 2 j (+1)] for barrier j. The product build has
+// no stamps.
 #ifdef MSHA_CHAIN2_STAMPS
 __device__ uint64_t* g_chain2_stamps;
-#define MSHA_C2_STAMP(k)                                                                        \
+#define MSHA_C2_BARRIER(j)                                                                      \
   {                                                                                             \
-    const uint64_t k_ = (k);                                                                    \
-    if (blockIdx.x == 0 && lane == 0 && k_ < 4096)                                              \
-      g_chain2_stamps[wave * 4096 + k_] = __builtin_amdgcn_s_memtime();                         \
+    const uint64_t j_ = (j);                                                                    \
+    if (blockIdx.x == 0 && lane == 0 && j_ < 2047)                                              \
+      g_chain2_stamps[wave * 4096 + 2 * j_] = __builtin_amdgcn_s_memtime();                     \
+    __syncthreads();                                                                            \
+    if (blockIdx.x == 0 && lane == 0 && j_ < 2047)                                              \
+      g_chain2_stamps[wave * 4096 + 2 * j_ + 1] = __builtin_amdgcn_s_memtime();                 \
   }
 #else
-#define MSHA_C2_STAMP(k)
+#define MSHA_C2_BARRIER(j) __syncthreads();
 #endif
-
-// K+W slots of the two-lane chain: a ring the producer fills up to kC2Slots - 1
-// blocks ahead of the consumers' compute, synchronised by LDS counters (the
-// producer publishes s_ready = blocks written, each consumer s_done = blocks it
-// has read) instead of a workgroup barrier per block: a barrier made producer
-// and consumers meet every block, and its release cost ~300-400 shader cycles a
-// block on the chain (tools/chain2_anatomy.hip).
-constexpr unsigned kC2Slots = 4;
 
 // Also AUTO's kernel for launches of at most 64 messages per CU (a call of a
 // few actions at low load: one chain's latency is the call's), where every
@@ -1005,8 +980,8 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
                                                        uint32_t* __restrict__ err,
                                                        const uint32_t* __restrict__ limit) {
   // [slot][quad t/4][message] x 16 B, then 16 zero quads (the a-lanes' K+W)
-  __shared__ uint4 kw[kC2Slots][kCoopSlotQuads * 64 + kCoopSlotQuads];
-  __shared__ uint32_t s_nb, s_ready, s_done[2];
+  __shared__ uint4 kw[2][kCoopSlotQuads * 64 + kCoopSlotQuads];
+  __shared__ uint32_t s_nb;
   if (EXCL) asm volatile("" ::: "v255", "a255");  // exclusive CU (see k_digest_coop EXCL)
   if (EXCL) __builtin_amdgcn_s_setprio(3);
   const unsigned lane = threadIdx.x & 63;
@@ -1040,8 +1015,8 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   }
   const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
   const uint32_t nb = nfull + (r < 56 ? 1 : 2);
-  if (threadIdx.x == 0) s_nb = s_ready = s_done[0] = s_done[1] = 0;
-  if (threadIdx.x < kC2Slots * kCoopSlotQuads) kw[threadIdx.x >> 4][kCoopSlotQuads * 64 + (threadIdx.x & 15)] =
+  if (threadIdx.x == 0) s_nb = 0;
+  if (threadIdx.x < 2 * kCoopSlotQuads) kw[threadIdx.x >> 4][kCoopSlotQuads * 64 + (threadIdx.x & 15)] =
       make_uint4(0, 0, 0, 0);
   __syncthreads();
   if (producer && active) atomicMax(&s_nb, nb);
@@ -1061,18 +1036,10 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
         length_block(L, w);
       }
       if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
-      MSHA_C2_STAMP(2 * b)
-      if (b >= kC2Slots) {  // slot b % kC2Slots held block b - kC2Slots: both consumers have read it?
-        const uint32_t need = b - kC2Slots + 1;
-        while (min(__hip_atomic_load(&s_done[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP),
-                   __hip_atomic_load(&s_done[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) < need)
-          __builtin_amdgcn_s_sleep(1);
-      }
-      MSHA_C2_STAMP(2 * b + 1)
-      schedule_kw(w, &kw[b % kC2Slots][lane]);
-      // release: the slot's writes land before the count that publishes them
-      if (lane == 0) __hip_atomic_store(&s_ready, b + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+      schedule_kw(w, &kw[b & 1][lane]);
+      MSHA_C2_BARRIER(b)  // barrier b: slot b & 1 holds block b
     }
+    MSHA_C2_BARRIER(NB)  // barrier NB: the consumers' last (they wait one block ahead)
   } else {
     // e-side: e f g h, rotates 6 11 25; a-side: a b c d, rotates 2 13 22
     uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
@@ -1088,24 +1055,24 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     // register sets alternate by unrolling the block loop twice, so nothing is
     // copied between blocks.
     uint4 ka[16], kb[16];
-    MSHA_C2_STAMP(0)
-    while (__hip_atomic_load(&s_ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < 1)  // block 0 written
-      __builtin_amdgcn_s_sleep(1);
-    MSHA_C2_STAMP(1)
+    MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds block 0
 #pragma unroll
     for (int q = 0; q < 16; ++q) ka[q] = kw[0][col + q * qstride];
     for (uint32_t b = 0; b < NB; ++b) {
-      MSHA_DBLOCK(ka, kb)  // (a read past the last block, of a slot never rewritten, is unused)
+      MSHA_C2_BARRIER(b + 1)
+      unsigned ns = (b + 1) & 1;  // a read past the last block is harmless (unused)
+      MSHA_DBLOCK(ka, kb)
       if (++b == NB) break;
+      MSHA_C2_BARRIER(b + 1)
+      ns = (b + 1) & 1;
       MSHA_DBLOCK(kb, ka)
     }
   }
 }
 #undef MSHA_DBLOCK
-#undef MSHA_PF
 #undef MSHA_D4
 #undef MSHA_ASM_ROUND
-#undef MSHA_C2_STAMP
+#undef MSHA_C2_BARRIER
 
 // Uniform layout: message i is arena[i*stride : i*stride + msg_len].
 template <int MODE>

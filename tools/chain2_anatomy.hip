@@ -72,19 +72,16 @@ int main(int argc, char** argv) {
   CHECK(hipEventElapsedTime(&ms, e0, e1));
   std::vector<uint64_t> h(3 * 4096);
   CHECK(hipMemcpy(h.data(), stamps, 8 * h.size(), hipMemcpyDeviceToHost));
-  // stamps k: consumers 2 (b+1) / 2 (b+1) + 1 = before / after waiting for block
-  // b+1's K+W (inside block b, after its first four rounds); producer 2 b / 2 b + 1
-  // = before / after waiting for block b's slot to be free
   auto st = [&](int wave, uint64_t j, int after) { return (double)h[wave * 4096 + 2 * j + after]; };
   const uint64_t nb = std::min<uint64_t>(NB, 2040);
   std::vector<double> c_comp, c_wait, p_comp, p_wait;
   for (uint64_t b = 1; b + 2 < nb; ++b) {  // steady state: skip the first and last blocks
-    c_comp.push_back(st(1, b + 2, 0) - st(1, b + 1, 1));  // one block's period minus the wait
+    c_comp.push_back(st(1, b + 2, 0) - st(1, b + 1, 1));  // block b: after barrier b+1 .. barrier b+2
     c_wait.push_back(st(1, b + 1, 1) - st(1, b + 1, 0));
-    p_comp.push_back(st(0, b, 0) - st(0, b - 1, 1));
+    p_comp.push_back(st(0, b, 0) - st(0, b - 1, 1));      // block b's slot: after barrier b-1 .. barrier b
     p_wait.push_back(st(0, b, 1) - st(0, b, 0));
   }
-  const double total_ticks = st(1, nb - 1, 1) - st(1, 0, 0);
+  const double total_ticks = st(1, nb, 1) - st(1, 0, 0);
   const double ghz = total_ticks / (ms * 1e-3) / 1e9;  // approx: ticks over the launch's event time
   printf("{\"blocks\": %llu, \"kernel_ms\": %.4f, \"us_per_block\": %.4f, \"ticks_per_block\": %.1f, "
          "\"approx_clock_ghz\": %.3f, \"consumer_compute_ticks_median\": %.1f, \"consumer_compute_ticks_mean\": %.1f, "
