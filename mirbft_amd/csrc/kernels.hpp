@@ -119,8 +119,9 @@ struct FoldArgs {
   const uint64_t* off;
   const uint64_t* len;
   uint64_t n = 0;
-  uint32_t* table = nullptr;  // tmask + 1 zeroed entries; null: no folding
+  uint64_t* table = nullptr;  // tmask + 1 slots (epoch << 32 | message + 1); null: no folding
   uint64_t tmask = 0;
+  uint32_t epoch = 1;         // this call's tag: a slot of another epoch is empty (never 0)
   uint32_t* rep = nullptr;    // n (with table): the lane message i's digest comes from
   uint64_t* tmax = nullptr;   // (with table) ceil(n / 4096): largest offset before each tile
   uint32_t* cnt;              // kFoldBuckets zeroed counters -> bucket starts

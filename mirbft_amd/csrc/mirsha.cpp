@@ -238,6 +238,7 @@ struct Device {
   // representatives, bucket counters, lane order, [lanes | head]; the head of
   // long chains runs on side_stream, forked from and joined to the caller's
   DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_info;
+  uint32_t f_epoch = 0;  // the alias table's epoch tag of the last folded call (plan.hip fold_claim)
   DevBuf probe;  // msha_clock_probe: stamps + sink
   // direct path heads (launch_head): their digests, lane-indexed; read back with
   // their lanes' digest slots into h_head ([digests | slots])
@@ -2713,8 +2714,17 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     d.f_cnt.ensure(4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets);  // counters, then FoldArgs::big
     d.f_order.ensure(4 * n);
     d.f_info.ensure(8);
+    bool clear_table = false;
     if (fold) {
-      d.f_table.ensure(4 * cap);
+      // epoch-tagged slots (plan.hip fold_claim): cleared only when the table
+      // is (re)allocated -- hipMalloc does not zero -- or the epoch wraps
+      const void* before = d.f_table.p;
+      d.f_table.ensure(8 * cap);
+      if (d.f_table.p != before || d.f_epoch == 0xFFFFFFFFu) {
+        clear_table = true;
+        d.f_epoch = 0;
+      }
+      ++d.f_epoch;
       d.f_rep.ensure(4 * n);
       d.f_tmax.ensure(8 * ((n + 4095) / 4096));
     }
@@ -2738,15 +2748,16 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       HIPCHK(hipStreamWaitEvent(d.side_stream, d.ev_fork, 0));
       ps = d.side_stream;
     }
-    if (fold) HIPCHK(hipMemsetAsync(d.f_table.p, 0, 4 * cap, ps));
+    if (clear_table) HIPCHK(hipMemsetAsync(d.f_table.p, 0, d.f_table.cap, ps));
     HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets, ps));
-    HIPCHK(hipMemsetAsync(d.f_order.p, 0xFF, 4 * n, ps));  // kNoLane
+    // (the order's positions past the last lane are filled by k_fold_scatter)
     msha::FoldArgs fa;
     fa.off = d_off;
     fa.len = d_len;
     fa.n = n;
-    fa.table = fold ? d.f_table.as<uint32_t>() : nullptr;
+    fa.table = fold ? d.f_table.as<uint64_t>() : nullptr;
     fa.tmask = cap - 1;
+    fa.epoch = d.f_epoch;
     fa.rep = fold ? d.f_rep.as<uint32_t>() : nullptr;
     fa.tmax = fold ? d.f_tmax.as<uint64_t>() : nullptr;
     fa.cnt = d.f_cnt.as<uint32_t>();

@@ -284,12 +284,13 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t st) {
 //   k_fold_tilemax, k_fold_tilescan, k_fold_insert   (folding only) messages
 //                   that may repeat an earlier payload claim (off, len) in an
 //                   open-addressing table; the claimer is the key's lane (any one
-//                   will do: the digest is the same), rep[i] = that lane
-//   k_fold_keys     lanes counted per descending block-count bucket
+//                   will do: the digest is the same), rep[i] = that lane; and the
+//                   lanes counted per descending block-count bucket
+//   k_fold_keys     (no folding) the same count, every message a lane
 //   k_fold_scan     one workgroup: bucket starts, lanes, the batch's lane blocks,
 //                   its longest chain, and the head: lanes whose chain on the
 //                   lane kernel would outlast the launch's floor (FoldArgs)
-//   k_fold_scatter  order[position] = message
+//   k_fold_scatter  order[position] = message; kNoLane past the last lane
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ uint32_t fold_bucket(uint64_t blocks) {  // ascending class
   if (blocks < 4096) return (uint32_t)blocks;
@@ -350,23 +351,65 @@ __global__ __launch_bounds__(1024) void k_fold_tilescan(FoldArgs a, uint64_t til
   }
 }
 
+// The alias table's slots are 64-bit (epoch << 32 | message + 1): a slot whose
+// epoch is not this call's is empty, so the table is never cleared between
+// calls (the host clears it only when it is (re)allocated or the epoch wraps).
 __device__ __forceinline__ uint32_t fold_claim(const FoldArgs& a, uint64_t i, uint64_t o, uint64_t l) {
   uint64_t h = plan_hash(o, l) & a.tmask;
-  const uint32_t me = (uint32_t)i + 1;  // 0 = empty slot
+  const uint64_t ep = (uint64_t)a.epoch << 32;
+  const uint64_t me = ep | ((uint64_t)i + 1);
   for (;;) {
-    // a plain read first: a claimed slot never empties, and a hot key (one
-    // payload named by thousands of messages) then costs a cached read
-    uint32_t v = __hip_atomic_load(&a.table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (v == 0) v = atomicCAS(&a.table[h], 0u, me);
-    if (v == 0) return (uint32_t)i;
-    const uint64_t j = v - 1;
+    // a plain read first: a claimed slot never empties within a call, and a hot
+    // key (one payload named by thousands of messages) then costs a cached read
+    uint64_t v = __hip_atomic_load(&a.table[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if ((v & ~0xFFFFFFFFull) != ep) {  // empty: claim it
+      const uint64_t prev = atomicCAS(reinterpret_cast<unsigned long long*>(&a.table[h]), v, me);
+      if (prev == v) return (uint32_t)i;
+      v = prev;
+      if ((v & ~0xFFFFFFFFull) != ep) continue;  // not claimed by this call: look again
+    }
+    const uint64_t j = (v & 0xFFFFFFFFull) - 1;
     if (a.off[j] == o && a.len[j] == l) return (uint32_t)j;
     h = (h + 1) & a.tmask;
   }
 }
 
+// Lanes counted per descending block-count key in a tile's LDS histogram (and,
+// for the power-of-two classes, their largest block count and block sum), then
+// flushed to the global counters: one global atomic per key present in the tile.
+struct FoldHist {
+  uint32_t n[kFoldBuckets];
+  unsigned long long bmax[kFoldBigBuckets], bsum[kFoldBigBuckets];
+};
+__device__ __forceinline__ void fold_hist_clear(FoldHist& h) {
+  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x) h.n[j] = 0;
+  if (threadIdx.x < kFoldBigBuckets) h.bmax[threadIdx.x] = h.bsum[threadIdx.x] = 0;
+}
+__device__ __forceinline__ void fold_hist_add(FoldHist& h, uint64_t len) {
+  const uint64_t blocks = dev_blocks_for(len);
+  const uint32_t k = kFoldBuckets - 1 - fold_bucket(blocks);
+  atomicAdd(&h.n[k], 1u);
+  if (k < kFoldBigBuckets) {  // >= 4,096 blocks (1/4 MiB): rare
+    atomicMax(&h.bmax[k], (unsigned long long)blocks);
+    atomicAdd(&h.bsum[k], (unsigned long long)blocks);
+  }
+}
+__device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h) {
+  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
+    if (h.n[j]) atomicAdd(&a.cnt[j], h.n[j]);
+  if (threadIdx.x < kFoldBigBuckets && h.bsum[threadIdx.x]) {
+    atomicMax(reinterpret_cast<unsigned long long*>(&a.big[threadIdx.x]), h.bmax[threadIdx.x]);
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.big[kFoldBigBuckets + threadIdx.x]), h.bsum[threadIdx.x]);
+  }
+}
+
+// Also counts the tile's lanes into the bucket histogram (what k_fold_keys
+// does without folding): a fresh message is its own lane, a candidate is one
+// when its claim returns itself -- so the lanes' metadata is read once.
 __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   __shared__ uint64_t part[256];
+  __shared__ FoldHist hist;
+  fold_hist_clear(hist);
   const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanItems;
   uint64_t o[kPlanItems];
   uint64_t m = 0;
@@ -398,18 +441,25 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     const uint64_t i = base + r;
     if (i >= a.n) break;
     const bool fresh = o[r] > run || (first_ever && r == 0);  // above every earlier offset
-    if (fresh)
+    if (fresh) {
       a.rep[i] = (uint32_t)i;
-    else
+      fold_hist_add(hist, a.len[i]);
+    } else {
       cand[atomicAdd(&ncand, 1u)] = (uint32_t)(i - (uint64_t)blockIdx.x * kPlanTile);
+    }
     run = max(run, o[r]);
   }
   __syncthreads();
   const uint64_t tile0 = (uint64_t)blockIdx.x * kPlanTile;
   for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
     const uint64_t i = tile0 + cand[c];
-    a.rep[i] = fold_claim(a, i, a.off[i], a.len[i]);
+    const uint64_t l = a.len[i];
+    const uint32_t rp = fold_claim(a, i, a.off[i], l);
+    a.rep[i] = rp;
+    if (rp == (uint32_t)i) fold_hist_add(hist, l);
   }
+  __syncthreads();
+  fold_hist_flush(a, hist);
 }
 
 // The fold planner's keys are few (kFoldBuckets), so a tile counts them in a
@@ -421,33 +471,19 @@ constexpr uint32_t kFoldItems = kPlanItems;          // messages per thread
 constexpr uint32_t kFoldTile = 256 * kFoldItems;     // messages per workgroup
 static_assert(kFoldTile <= 4096 && (kFoldBuckets << 12) < kEmptyKey, "scatter packs key << 12 | rank");
 
+// Without folding every message is a lane (with folding k_fold_insert counts).
 __global__ __launch_bounds__(256) void k_fold_keys(FoldArgs a) {
-  __shared__ uint32_t hist[kFoldBuckets];
-  __shared__ unsigned long long bmax[kFoldBigBuckets], bsum[kFoldBigBuckets];
-  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x) hist[j] = 0;
-  if (threadIdx.x < kFoldBigBuckets) bmax[threadIdx.x] = bsum[threadIdx.x] = 0;
+  __shared__ FoldHist hist;
+  fold_hist_clear(hist);
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
 #pragma unroll 4
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    if (i < a.n && (!a.table || a.rep[i] == (uint32_t)i)) {
-      const uint64_t blocks = dev_blocks_for(a.len[i]);
-      const uint32_t k = kFoldBuckets - 1 - fold_bucket(blocks);
-      atomicAdd(&hist[k], 1u);
-      if (k < kFoldBigBuckets) {  // >= 4,096 blocks (1/4 MiB): rare
-        atomicMax(&bmax[k], (unsigned long long)blocks);
-        atomicAdd(&bsum[k], (unsigned long long)blocks);
-      }
-    }
+    if (i < a.n) fold_hist_add(hist, a.len[i]);
   }
   __syncthreads();
-  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
-    if (hist[j]) atomicAdd(&a.cnt[j], hist[j]);
-  if (threadIdx.x < kFoldBigBuckets && bsum[threadIdx.x]) {
-    atomicMax(reinterpret_cast<unsigned long long*>(&a.big[threadIdx.x]), bmax[threadIdx.x]);
-    atomicAdd(reinterpret_cast<unsigned long long*>(&a.big[kFoldBigBuckets + threadIdx.x]), bsum[threadIdx.x]);
-  }
+  fold_hist_flush(a, hist);
 }
 
 // Key k's longest chain and its c lanes' blocks: exact below 4,096 blocks (one
@@ -594,6 +630,10 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
     if (item[r] == kEmptyKey) continue;
     a.order[hist[item[r] >> 12] + (item[r] & 0xFFFu)] = (uint32_t)(base + r * 256 + threadIdx.x);
   }
+  // positions past the last lane (the folded aliases' share) hold kNoLane
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t q = a.info[0] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += stride)
+    a.order[q] = kNoLane;
 }
 
 __global__ __launch_bounds__(256) void k_fold_fill(const uint32_t* __restrict__ rep, uint64_t n,
@@ -617,7 +657,7 @@ hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(k_fold_insert, dim3(ptiles), dim3(256), 0, st, a);
   }
   const unsigned ftiles = (unsigned)((a.n + kFoldTile - 1) / kFoldTile);
-  hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
+  if (!a.table) hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(k_fold_scatter, dim3(ftiles), dim3(256), 0, st, a);
   return hipGetLastError();
