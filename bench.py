@@ -654,6 +654,8 @@ def main():
             "config": {"workload": w.name, "config": args.config, "messages_per_gpu": w.n,
                        "message_bytes_per_gpu": w.message_bytes, "blocks_per_gpu": w.blocks,
                        "hashed_blocks_per_gpu": hashed_blocks(w, args.config),
+                       "max_blocks_per_message": int((int(w.len.max()) >> 6) + (1 if (int(w.len.max()) & 63) < 56
+                                                                                  else 2)) if w.n else 0,
                        "parallelism": f"independent shards x{world}"},
             "gbps_hashed": gbps,
             "kernel_ms_mean": kern_ms,

@@ -102,7 +102,7 @@ def bench_line(run):
     return json.loads(lines[-1])
 
 
-def kernel_entry(k, sq, sq2, fe, wr, cf):
+def kernel_entry(k, sq, sq2, fe, wr, cf, max_blocks=0):
     rows = sq[k]
     ns = mean_ns(rows)
     grbm = mean(rows, "GRBM_GUI_ACTIVE")
@@ -117,12 +117,14 @@ def kernel_entry(k, sq, sq2, fe, wr, cf):
          "valu_busy_pct": 100 * active / CUS / cyc if cyc else None,
          "wait_any_share": mean(rows, "SQ_WAIT_ANY") / wave_cyc if wave_cyc else None}
     base = k.split("<")[0].split("::")[-1]
-    if base in WAVES_PER_WG and waves:
-        # a head: one workgroup per CU, so its figures over the CUs it holds
-        own = waves / WAVES_PER_WG[base]
-        e["occupied_cus"] = own
-        e["valu_busy_pct_own_cus"] = 100 * active / own / cyc if cyc else None
-        e["simd_cycles_per_valu_instr_own_simds"] = cyc * own * 4 / insts if insts else None
+    if base in WAVES_PER_WG and max_blocks:
+        # a head: its time is its longest chain's (max_blocks blocks, serial);
+        # every workgroup of the launch is dispatched, those past the head's
+        # lanes exit at once, so per-CU occupancy figures would mislead
+        e["chain_blocks"] = max_blocks
+        e["us_per_chain_block"] = ns / 1e3 / max_blocks
+        e["cycles_per_chain_block"] = cyc / max_blocks
+        e["wave_valu_instr_per_chain_block"] = insts / max_blocks
     if sq2 and k in sq2:
         r2 = sq2[k]
         thr, act2 = mean(r2, "SQ_THREAD_CYCLES_VALU"), mean(r2, "SQ_ACTIVE_INST_VALU")
@@ -148,8 +150,8 @@ def main():
                                        "per block; the step's hash kernels)",
                "simd_cycles_per_valu_instr": "clock cycles x 1024 SIMDs / SQ_INSTS_VALU",
                "valu_busy_pct": "VALUBusy = 100 x SQ_ACTIVE_INST_VALU / 256 CUs / (GRBM_GUI_ACTIVE / 8)",
-               "valu_busy_pct_own_cus": "heads (one workgroup per CU): the same over the CUs the kernel holds "
-                                        "(SQ_WAVES / waves per workgroup)",
+               "cycles_per_chain_block": "heads: GRBM clock cycles of the launch / its longest chain's blocks "
+                                         "(the head's time is that chain's)",
                "valu_utilization_pct": "VALUUtilization = 100 x SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)",
                "int32_share": "SQ_INSTS_VALU_INT32 / SQ_INSTS_VALU",
                "algorithmic_tops": "1400 x hashed blocks / kernel ns (bench roofline.achieved); frac vs 78.64 T",
@@ -167,7 +169,7 @@ def main():
         cfg = b["config"]
         blocks, msgs = cfg["blocks_per_gpu"], cfg["messages_per_gpu"]
         hashed = cfg.get("hashed_blocks_per_gpu", blocks)
-        kernels = {k: kernel_entry(k, sq, sq2, fe, wr, cf) for k in sq}
+        kernels = {k: kernel_entry(k, sq, sq2, fe, wr, cf, cfg.get("max_blocks_per_message", 0)) for k in sq}
         # msha_clock_probe runs after the timed steps (bench.py effective_clock_ghz): not part of a step
         probe = {k: kernels.pop(k) for k in list(kernels) if "k_clock_probe" in k}
         hash_k = [k for k in kernels if "k_digest" in k]
@@ -202,9 +204,9 @@ def main():
               f"  frac {e['roofline_frac']:.3f}  hbm x{e.get('hbm_over_algorithmic', 0):.2f}")
         for k, v in e["kernels"].items():
             if k != e["kernel"]:
-                own = v.get("valu_busy_pct_own_cus")
+                ch = v.get("cycles_per_chain_block")
                 print(f"    {k[:44]:44s} {v['us']:8.1f} us  busy {v['valu_busy_pct'] or 0:5.1f}%"
-                      + (f" (own CUs {own:5.1f}%, {v['occupied_cus']:.0f} CUs)" if own is not None else "")
+                      + (f" (chain: {v['us_per_chain_block']:.3f} us, {ch:.0f} cycles per block)" if ch else "")
                       + f"  hbm {v.get('hbm_bytes', 0) / 1e6:8.1f} MB")
 
 
