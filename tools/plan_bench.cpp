@@ -19,9 +19,13 @@ bool plan_split(uint64_t, int, int, SplitPlan*, int) { return false; }
 hipError_t launch_plan(const PlanArgs&, hipStream_t) { return hipErrorNotSupported; }
 hipError_t launch_digest_batch(const uint8_t*, const uint64_t*, const uint64_t*, const uint32_t*,
                                const uint32_t*, uint64_t, uint8_t*, uint32_t*, int, int, hipStream_t,
-                               const SplitPlan*, LaunchKind*) {
+                               const SplitPlan*, LaunchKind*, const LaneGate*) {
   return hipErrorNotSupported;
 }
+hipError_t launch_fold_plan(const FoldArgs&, hipStream_t) { return hipErrorNotSupported; }
+hipError_t launch_fold_fill(const uint32_t*, uint64_t, uint8_t*, hipStream_t) { return hipErrorNotSupported; }
+hipError_t launch_clock_probe(uint32_t, uint32_t, uint64_t*, uint32_t*, hipStream_t) { return hipErrorNotSupported; }
+bool uses_coop(uint64_t, int, int) { return false; }
 hipError_t launch_digest_uniform(const uint8_t*, uint64_t, uint64_t, uint64_t, uint8_t*, uint32_t*, int,
                                  hipStream_t, LaunchKind*) {
   return hipErrorNotSupported;
@@ -102,7 +106,8 @@ int main(int argc, char** argv) {
           tl_pool = k > 1 ? pools[s].get() : nullptr;
           const uint64_t a = bounds[s], m = bounds[s + 1] - a;
           std::vector<uint8_t> mark(nG, 0);
-          const ShardSpan sh = stage_and_mark(off.data() + a, len.data() + a, m, glo, gs, nullptr, nullptr, mark);
+          const ShardSpan sh = stage_and_mark(off.data() + a, len.data() + a, m, glo, gs, nullptr, nullptr, mark,
+                                              long_chain_blocks(sc.bmax));
           std::vector<uint64_t> gmap(sh.g1 - sh.g0 + 1);
           build_gmap(mark, sh.g0, gmap.size(), gs, gmap.data());
           done[s] = now_ms() - t1;
