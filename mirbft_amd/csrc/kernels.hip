@@ -766,6 +766,25 @@ __device__ __forceinline__ void schedule_kw(uint32_t (&w)[16], uint4* __restrict
   }
 }
 
+// k_digest_chain2's packing (its consumers alternate E- and A-rounds): quad 2g
+// holds the K+W words of rounds 8g, 8g+2, 8g+4, 8g+6 (the e-lanes'), quad 2g+1
+// those of rounds 8g+1, ..., 8g+7 (the a-lanes').
+__device__ __forceinline__ void schedule_kw_eo(uint32_t (&w)[16], uint4* __restrict__ slot) {
+  constexpr uint32_t K[64] = {MSHA_K_TABLE};
+#pragma unroll
+  for (int g = 0; g < 8; ++g) {
+    uint32_t x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int t = 8 * g + j;
+      if (t >= 16) MSHA_SCHED(w, t);
+      x[j] = w[t & 15] + K[t];
+    }
+    slot[(2 * g) * 64] = make_uint4(x[0], x[2], x[4], x[6]);
+    slot[(2 * g + 1) * 64] = make_uint4(x[1], x[3], x[5], x[7]);
+  }
+}
+
 // Workgroup = 4 waves serving 128 messages: waves 0/1 consume (rounds) for
 // message groups 0/1, waves 2/3 produce (schedules) for the same groups. A
 // workgroup's waves take SIMDs in the cyclic order 0->2->1->3, so each wave
@@ -880,27 +899,76 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
 // (a b c d). One v_alignbit x3 + xor3 then computes Sigma1 in the e-lane and
 // Sigma0 in the a-lane (per-lane rotate amounts), Ch and Maj are one bitop3
 // each, and the two new words come from two row_mirror DPP adds that write only
-// their side's lanes (bank_mask) -- 11 instructions a round:
-//   e-lane  U = Sig1 + Ch + (h + KW) = T1,   e' = mirror(d) + T1
-//   a-lane  T = Sig0 + Maj (its KW is 0) = T2, a' = mirror(T1) + T2
+// their side's lanes (bank_mask) -- 11 instructions a round (below):
+//   e' = mirror(d) + T1,   a' = mirror(T1) + T2
 // Register-resident, one wave alone on its SIMD: 21.1 against 23.7 ns a round
 // (tools/chain_dpp_microbench.hip, profiles/r03_chain_dpp/). Workgroup = one
 // producer wave (64 messages: loads, padding, K+W schedules into LDS, as in
 // k_digest_coop) and two consumer waves of 32 messages; EXCL as above (the
 // head's CUs hold nothing else); each lane stores its side's four digest words.
-// The rounds are inline asm (MSHA_D4 below): a DPP read of a VGPR needs 2 wait
+// The rounds are inline asm (MSHA_DQ below): a DPP read of a VGPR needs 2 wait
 // states after the VALU write of it, and the compiler's hazard recognizer does
 // not look inside asm text, so the asm orders its own instructions to satisfy
 // that, and tools/check_dpp_hazards.py checks every DPP of the built library.
 // ---------------------------------------------------------------------------
-// One round in asm (X Y Z W: this lane's side, newest to oldest; the new word
-// replaces W). Named operands: sh1-3 the lane's rotate amounts, k the lane's
-// K+W word (0 in a-lanes), s1 s2 s3 s sk c u m t scratch.
-#define MSHA_ASM_ROUND(X, Y, Z, W, K)                                                            \
+// The rounds in asm (X Y Z W: this lane's side, newest to oldest; the new word
+// replaces W). Both lanes of a message run the same instruction stream; what a
+// lane computes that its side does not need is simply not used.
+//  E-round (11 instructions; K is read in the e-lanes only):
+//    s = Sigma (3 v_alignbit + xor3; Sigma1 in the e-lanes, Sigma0 in the
+//    a-lanes), c = Ch, m = Maj (one bitop3 each), u = s + W + c, T1 = u + K
+//    (the e-lanes' W is h), t = s + m (T2 in the a-lanes), then two row_mirror
+//    DPP adds that write only their side's lanes (bank_mask):
+//    e' = mirror(d) + T1, a' = mirror(T1) + t.
+//  A-round (11 instructions; K is read in the a-lanes only): y = W + K (d + K
+//    in the a-lanes), s, c, m, u = s + W + c (Sigma1 + h + Ch in the e-lanes),
+//    t = s + K + m (Sigma0 + K + Maj in the a-lanes), then e' = mirror(y) + u
+//    and a' = mirror(u) + t -- the same two sums, K carried on the other side.
+// Rounds alternate E, A, E, A, ..., so each lane needs the K+W words of every
+// OTHER round: the producer packs rounds 8g, 8g+2, 8g+4, 8g+6 into the e-lanes'
+// quad and 8g+1, ..., 8g+7 into the a-lanes', and a consumer lane reads ONE
+// ds_read_b128 per 8 rounds (MSHA_CHAIN2_FORM 4). Round 3's consumer ran
+// E-rounds only, the a-lanes reading 16 zero quads a block to get K = 0: 16
+// reads a block instead of 8 (MSHA_CHAIN2_FORM 3, kept for the A/B). On a lone
+// wave a ds_read_b128 costs ~14 shader cycles of issue (one VALU slot plus its
+// 1 KiB return), 3.6 cycles a round at one per 4 rounds
+// (tools/round_issue_microbench.hip, profiles/r04_chain2_forms/). Named
+// operands: sh1-3 the lane's rotate amounts, K the round's K+W word, the rest
+// scratch.
+#ifndef MSHA_CHAIN2_FORM
+#define MSHA_CHAIN2_FORM 4
+#endif
+#define MSHA_ASM_SIGMA(X)                                                                        \
   "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh1]\n\t"                                       \
   "v_alignbit_b32 %[s2], %[" #X "], %[" #X "], %[sh2]\n\t"                                       \
   "v_alignbit_b32 %[s3], %[" #X "], %[" #X "], %[sh3]\n\t"                                       \
-  "v_bitop3_b32 %[s], %[s1], %[s2], %[s3] bitop3:0x96\n\t"                                      \
+  "v_bitop3_b32 %[s], %[s1], %[s2], %[s3] bitop3:0x96\n\t"
+#define MSHA_ASM_CHMAJ(X, Y, Z)                                                                  \
+  "v_bitop3_b32 %[c], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xca\n\t"                           \
+  "v_bitop3_b32 %[m], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xe8\n\t"
+// E-round. The second DPP reads T1 (sk) two instructions after writing it (t and
+// the first DPP between): the 2 wait states a DPP source needs after a VALU
+// write; the first reads W, written four rounds earlier.
+#define MSHA_ASM_EROUND(X, Y, Z, W, K)                                                           \
+  MSHA_ASM_SIGMA(X) MSHA_ASM_CHMAJ(X, Y, Z)                                                      \
+  "v_add3_u32 %[u], %[s], %[" #W "], %[c]\n\t"                                                    \
+  "v_add_u32 %[sk], %[u], %[" #K "]\n\t"                                                          \
+  "v_add_u32 %[t], %[s], %[m]\n\t"                                                                \
+  "v_add_u32_dpp %[" #W "], %[" #W "], %[sk] row_mirror row_mask:0xf bank_mask:0x3\n\t"          \
+  "v_add_u32_dpp %[" #W "], %[sk], %[t] row_mirror row_mask:0xf bank_mask:0xc\n\t"
+// A-round: y is written first, nine instructions before the DPP that reads it;
+// the second DPP reads u two instructions after writing it.
+#define MSHA_ASM_AROUND(X, Y, Z, W, K)                                                           \
+  "v_add_u32 %[y], %[" #W "], %[" #K "]\n\t"                                                      \
+  MSHA_ASM_SIGMA(X) MSHA_ASM_CHMAJ(X, Y, Z)                                                      \
+  "v_add3_u32 %[u], %[s], %[" #W "], %[c]\n\t"                                                    \
+  "v_add3_u32 %[t], %[s], %[" #K "], %[m]\n\t"                                                    \
+  "v_add_u32_dpp %[" #W "], %[y], %[u] row_mirror row_mask:0xf bank_mask:0x3\n\t"                \
+  "v_add_u32_dpp %[" #W "], %[u], %[t] row_mirror row_mask:0xf bank_mask:0xc\n\t"
+// Round 3's round (form 3): sk = Sigma + K (K 0 in the a-lanes), u = sk + W + Ch,
+// t = sk + Maj; the second DPP reads u three instructions after writing it.
+#define MSHA_ASM_ROUND3(X, Y, Z, W, K)                                                           \
+  MSHA_ASM_SIGMA(X)                                                                              \
   "v_add_u32 %[sk], %[s], %[" #K "]\n\t"                                                          \
   "v_bitop3_b32 %[c], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xca\n\t"                           \
   "v_add3_u32 %[u], %[sk], %[" #W "], %[c]\n\t"                                                   \
@@ -908,43 +976,56 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
   "v_add_u32 %[t], %[sk], %[m]\n\t"                                                               \
   "v_add_u32_dpp %[" #W "], %[" #W "], %[u] row_mirror row_mask:0xf bank_mask:0x3\n\t"           \
   "v_add_u32_dpp %[" #W "], %[u], %[t] row_mirror row_mask:0xf bank_mask:0xc\n\t"
-// Four rounds from quad q of cur; the same quad of the NEXT block is read from
-// LDS slot nxt meanwhile, so its latency hides under the rounds. The four
-// rounds are ONE asm statement: a lone wave issues one instruction per ~4.6
-// cycles whatever it is, and the compiler puts an s_nop after every asm
-// statement whose output the next VALU instruction reads (it cannot see
-// whether the asm ended in a dst-forwarding instruction) -- with a statement
-// per round that was 2 s_nops a round, 13 issue slots instead of 11 (+16 % a
-// block; tools/chain2_anatomy.hip). Inside, every DPP read is hazard-free by
-// construction: a round's second DPP reads u three instructions after writing
-// it (m, t and the first DPP between), and its first DPP reads W, written four
-// rounds earlier (tools/check_dpp_hazards.py checks the built library).
-#define MSHA_D4(cur, nxt, q)                                                                     \
+#define MSHA_ASM_OPERANDS                                                                        \
+  : [X] "+v"(X), [Y] "+v"(Y), [Z] "+v"(Z), [W] "+v"(W), [s1] "=&v"(s1_), [s2] "=&v"(s2_),      \
+    [s3] "=&v"(s3_), [s] "=&v"(s_), [sk] "=&v"(sk_), [c] "=&v"(c_), [u] "=&v"(u_), [m] "=&v"(m_), \
+    [t] "=&v"(t_), [y] "=&v"(y_)                                                                 \
+  : [sh1] "v"(sh1), [sh2] "v"(sh2), [sh3] "v"(sh3), [k0] "v"(v_.x), [k1] "v"(v_.y),              \
+    [k2] "v"(v_.z), [k3] "v"(v_.w)
+// One K+W quad of cur: 8 rounds (form 4) or 4 (form 3) in ONE asm statement --
+// a lone wave issues one instruction per ~4.1-4.6 cycles whatever it is, and
+// the compiler puts an s_nop after every asm statement whose output the next
+// VALU instruction reads (it cannot see whether the asm ended in a
+// dst-forwarding instruction): a statement per round cost 2 s_nops a round
+// (+16 % a block; tools/chain2_anatomy.hip). The same quad of the NEXT block is
+// read from LDS slot nxt meanwhile, so its latency hides under the rounds.
+// tools/check_dpp_hazards.py checks every DPP of the built library.
+#if MSHA_CHAIN2_FORM == 4
+constexpr int kC2Quads = 8;  // K+W quads a consumer lane reads per block
+#define MSHA_DQ(cur, nxt, q)                                                                     \
   {                                                                                              \
     const uint4 v_ = cur[q];                                                                     \
     nxt[q] = kw[ns][col + (q) * qstride];                                                        \
-    uint32_t s1_, s2_, s3_, s_, sk_, c_, u_, m_, t_;                                             \
-    asm volatile(MSHA_ASM_ROUND(X, Y, Z, W, k0) MSHA_ASM_ROUND(W, X, Y, Z, k1)                   \
-                 MSHA_ASM_ROUND(Z, W, X, Y, k2) MSHA_ASM_ROUND(Y, Z, W, X, k3)                   \
-                 : [X] "+v"(X), [Y] "+v"(Y), [Z] "+v"(Z), [W] "+v"(W), [s1] "=&v"(s1_),          \
-                   [s2] "=&v"(s2_), [s3] "=&v"(s3_), [s] "=&v"(s_), [sk] "=&v"(sk_), [c] "=&v"(c_), \
-                   [u] "=&v"(u_), [m] "=&v"(m_), [t] "=&v"(t_)                                   \
-                 : [sh1] "v"(sh1), [sh2] "v"(sh2), [sh3] "v"(sh3), [k0] "v"(v_.x), [k1] "v"(v_.y), \
-                   [k2] "v"(v_.z), [k3] "v"(v_.w));                                              \
+    uint32_t s1_, s2_, s3_, s_, sk_, c_, u_, m_, t_, y_;                                         \
+    asm volatile(MSHA_ASM_EROUND(X, Y, Z, W, k0) MSHA_ASM_AROUND(W, X, Y, Z, k0)                 \
+                 MSHA_ASM_EROUND(Z, W, X, Y, k1) MSHA_ASM_AROUND(Y, Z, W, X, k1)                 \
+                 MSHA_ASM_EROUND(X, Y, Z, W, k2) MSHA_ASM_AROUND(W, X, Y, Z, k2)                 \
+                 MSHA_ASM_EROUND(Z, W, X, Y, k3) MSHA_ASM_AROUND(Y, Z, W, X, k3)                 \
+                 MSHA_ASM_OPERANDS);                                                             \
   }
+#else
+constexpr int kC2Quads = 16;
+#define MSHA_DQ(cur, nxt, q)                                                                     \
+  {                                                                                              \
+    const uint4 v_ = cur[q];                                                                     \
+    nxt[q] = kw[ns][col + (q) * qstride];                                                        \
+    uint32_t s1_, s2_, s3_, s_, sk_, c_, u_, m_, t_, y_;                                         \
+    asm volatile(MSHA_ASM_ROUND3(X, Y, Z, W, k0) MSHA_ASM_ROUND3(W, X, Y, Z, k1)                 \
+                 MSHA_ASM_ROUND3(Z, W, X, Y, k2) MSHA_ASM_ROUND3(Y, Z, W, X, k3)                 \
+                 MSHA_ASM_OPERANDS);                                                             \
+    (void)y_;                                                                                    \
+  }
+#endif
 // One block b from cur (read during the previous block), reading block b+1's
 // K+W (slot ns) into nxt; the digest is stored after the message's last block.
-#define MSHA_DBLOCK(cur, nxt)                                                                          \
-  {                                                                                                    \
-    uint32_t X = H0, Y = H1, Z = H2, W = H3;                                                           \
-    MSHA_D4(cur, nxt, 0) MSHA_D4(cur, nxt, 1) MSHA_D4(cur, nxt, 2) MSHA_D4(cur, nxt, 3)              \
-    MSHA_D4(cur, nxt, 4) MSHA_D4(cur, nxt, 5) MSHA_D4(cur, nxt, 6) MSHA_D4(cur, nxt, 7)              \
-    MSHA_D4(cur, nxt, 8) MSHA_D4(cur, nxt, 9) MSHA_D4(cur, nxt, 10) MSHA_D4(cur, nxt, 11)            \
-    MSHA_D4(cur, nxt, 12) MSHA_D4(cur, nxt, 13) MSHA_D4(cur, nxt, 14) MSHA_D4(cur, nxt, 15)          \
-    H0 += X; H1 += Y; H2 += Z; H3 += W;                                                                \
-    if (active && b + 1 == nb)                                                                         \
-      *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =                                     \
-          make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));                                      \
+#define MSHA_DBLOCK(cur, nxt)                                                                    \
+  {                                                                                              \
+    uint32_t X = H0, Y = H1, Z = H2, W = H3;                                                     \
+    _Pragma("unroll") for (int q_ = 0; q_ < kC2Quads; ++q_) MSHA_DQ(cur, nxt, q_)                \
+    H0 += X; H1 += Y; H2 += Z; H3 += W;                                                          \
+    if (active && b + 1 == nb)                                                                   \
+      *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =                               \
+          make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));                                \
   }
 
 // Diagnostic build only (tools/chain2_anatomy.hip defines MSHA_CHAIN2_STAMPS):
@@ -1016,8 +1097,8 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
   const uint32_t nb = nfull + (r < 56 ? 1 : 2);
   if (threadIdx.x == 0) s_nb = 0;
-  if (threadIdx.x < 2 * kCoopSlotQuads) kw[threadIdx.x >> 4][kCoopSlotQuads * 64 + (threadIdx.x & 15)] =
-      make_uint4(0, 0, 0, 0);
+  if (MSHA_CHAIN2_FORM == 3 && threadIdx.x < 2 * kCoopSlotQuads)  // form 3: the a-lanes' zero quads
+    kw[threadIdx.x >> 4][kCoopSlotQuads * 64 + (threadIdx.x & 15)] = make_uint4(0, 0, 0, 0);
   __syncthreads();
   if (producer && active) atomicMax(&s_nb, nb);
   __syncthreads();
@@ -1036,7 +1117,10 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
         length_block(L, w);
       }
       if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
-      schedule_kw(w, &kw[b & 1][lane]);
+      if (MSHA_CHAIN2_FORM == 4)
+        schedule_kw_eo(w, &kw[b & 1][lane]);
+      else
+        schedule_kw(w, &kw[b & 1][lane]);
       MSHA_C2_BARRIER(b)  // barrier b: slot b & 1 holds block b
     }
     MSHA_C2_BARRIER(NB)  // barrier NB: the consumers' last (they wait one block ahead)
@@ -1045,19 +1129,24 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
     uint32_t H2 = eside ? 0x1f83d9abu : 0x3c6ef372u, H3 = eside ? 0x5be0cd19u : 0xa54ff53au;
     const uint32_t sh1 = eside ? 6 : 2, sh2 = eside ? 11 : 13, sh3 = eside ? 25 : 22;
+#if MSHA_CHAIN2_FORM == 4
+    // quad 2g: the e-lanes' K+W of rounds 8g, 8g+2, 8g+4, 8g+6; 2g+1: the a-lanes'
+    const unsigned col = (eside ? 0 : 64) + msg, qstride = 128;
+#else
     const unsigned col = eside ? msg : kCoopSlotQuads * 64;  // a-lanes read the zero quads
     const unsigned qstride = eside ? 64 : 1;
-    // Block b's K+W is read from LDS during block b-1's rounds (MSHA_D4), so a
+#endif
+    // Block b's K+W is read from LDS during block b-1's rounds (MSHA_DQ), so a
     // block starts on registers: barrier b+1 (the producer has written slot
     // (b+1) & 1) opens block b, whose rounds read it. The producer fills slot
     // b+2 -- the one block b-1 read, complete at barrier b+1 (__syncthreads
     // waits for every outstanding LDS read) -- while block b computes. Two
     // register sets alternate by unrolling the block loop twice, so nothing is
     // copied between blocks.
-    uint4 ka[16], kb[16];
+    uint4 ka[kC2Quads], kb[kC2Quads];
     MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds block 0
 #pragma unroll
-    for (int q = 0; q < 16; ++q) ka[q] = kw[0][col + q * qstride];
+    for (int q = 0; q < kC2Quads; ++q) ka[q] = kw[0][col + q * qstride];
     for (uint32_t b = 0; b < NB; ++b) {
       MSHA_C2_BARRIER(b + 1)
       unsigned ns = (b + 1) & 1;  // a read past the last block is harmless (unused)
@@ -1070,8 +1159,13 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   }
 }
 #undef MSHA_DBLOCK
-#undef MSHA_D4
-#undef MSHA_ASM_ROUND
+#undef MSHA_DQ
+#undef MSHA_ASM_OPERANDS
+#undef MSHA_ASM_ROUND3
+#undef MSHA_ASM_AROUND
+#undef MSHA_ASM_EROUND
+#undef MSHA_ASM_CHMAJ
+#undef MSHA_ASM_SIGMA
 #undef MSHA_C2_BARRIER
 
 // Uniform layout: message i is arena[i*stride : i*stride + msg_len].

@@ -138,7 +138,7 @@ struct FoldArgs {
   // throughput on a storm's mixed lanes ~6,500 per wave-block (uniform batches:
   // 5,700); a long chain on the lane kernel among loaded SIMDs ~8,000 (7,000 as
   // the oldest wave of a lightly loaded one); on the cooperative consumer, alone
-  // on its CU at top priority, ~4,200 (the two-lane head ~3,800). A sweep of the
+  // on its CU at top priority, ~4,200 (the two-lane head ~3,500 since round 4). A sweep of the
   // first two (MSHA_PLAN_LANE_CYCLES / MSHA_PLAN_WAVE_CYCLES,
   // profiles/r03_planned/calibration/): 8,000 / 6,500 ran c5 over 8 GPUs 3.00 ->
   // 2.85 ms, equal at 2 and 4. head_pct scales the head's term (A/B).
@@ -147,6 +147,7 @@ struct FoldArgs {
   uint32_t coop_cycles = 4200;
   uint32_t head_pct = 100;
   uint32_t head_per_wg = 128;    // messages per head workgroup (one CU each)
+  uint32_t tiebreak = 1;         // head-bound ties go to the cut with the most lane-kernel room (A/B: 0)
 };
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st);
 // out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.

@@ -2780,7 +2780,8 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     const bool two_lane = chain2_env == 2 || (chain2_env == 1 && fold);
     fa.head_per_wg = two_lane ? msha::kChain2MsgsPerWg : msha::kCoopMsgsPerWg;
     fa.head_cap = head ? (uint32_t)std::min<uint64_t>(n, (uint64_t)d.cus * fa.head_per_wg) : 0;
-    fa.coop_cycles = two_lane ? 3800 : 4200;
+    fa.coop_cycles = two_lane ? 3500 : 4200;  // two-lane head: 1,427 blocks in 2.04 ms at ~2.4 GHz (r04)
+    fa.tiebreak = (uint32_t)env_u64("MSHA_PLAN_TIEBREAK", 1);
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
     fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);

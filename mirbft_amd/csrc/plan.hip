@@ -501,15 +501,25 @@ __device__ __forceinline__ uint64_t key_sum_blocks(const FoldArgs& a, uint32_t k
 //   T(k) = max( h > 0 ? longest chain x coop_cycles : 0,
 //               remaining lane blocks / 64 / remaining SIMDs x wave_block_cycles,
 //               longest remaining chain x lane_cycles )
-// The cut with the smallest T wins (ties: the smaller head). head_pct scales
-// the head's term (A/B: 1 = a nearly free head, large = none).
+// The cut with the smallest T wins. Cuts whose T is the head's own term tie on
+// it, and among them the one whose lane-kernel part -- max(body, longest
+// remaining chain) -- leaves the most room wins: the cost is T + that part / 8
+// (ties after that: the smaller head; MSHA_PLAN_TIEBREAK=0: T alone, round 3's
+// rule -- equal on c5's slices, profiles/r04_tiebreak/). What moved c5 at 8
+// GPUs was the two-lane head's calibration (3,800 -> 3,500 cycles a block):
+// at 3,800 the model saw room under the head for the 652-block EpochChange
+// payloads on the lane kernel, whose chain then ended ~0.12 ms after the
+// head's (rocprofv3 timeline, profiles/r04_tiebreak/); folded slice 2.25-2.30
+// -> 2.15-2.16 ms. head_pct scales the head's term (A/B: 1 = a nearly free
+// head, large = none).
 __device__ __forceinline__ uint64_t head_cost(const FoldArgs& a, uint64_t h, uint64_t bh, uint64_t btot,
                                               uint64_t max_blocks, uint64_t next_blocks) {
   const uint64_t cus = a.simds / 4, hcus = (h + a.head_per_wg - 1) / a.head_per_wg;
   if (h > a.head_cap || hcus >= cus) return ~0ull;
   const uint64_t t_head = h ? max_blocks * a.coop_cycles / 100 * a.head_pct : 0;
   const uint64_t t_body = (btot - bh) * a.wave_block_cycles / (64ull * 4 * (cus - hcus));
-  return max(max(t_head, t_body), next_blocks * a.lane_cycles);
+  const uint64_t t_lanes = max(t_body, next_blocks * a.lane_cycles);
+  return max(t_head, t_lanes) + (a.tiebreak ? t_lanes / 8 : 0);
 }
 
 constexpr uint64_t kCostMax = (uint64_t(1) << 40) - 1;

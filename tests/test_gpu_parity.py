@@ -502,6 +502,18 @@ def test_pinned_arena_direct_upload(engine):
     assert engine.stats()["staged_calls"] == staged + 1
 
 
+def _mismatch(w, got, exp, e, what):
+    """What a failed comparison tells: how many digests differ, their messages'
+    block counts, and the call's figures (heads, lanes, split retries)."""
+    bad = np.nonzero(np.any(got != exp, axis=1))[0]
+    blocks = (w.len[bad].astype(np.int64) + 8) // 64 + 1
+    st = e.stats()
+    return {"what": what, "bad": int(bad.size), "first": bad[:8].tolist(),
+            "blocks": sorted(set(blocks.tolist()))[:16],
+            "split_retries": st.get("split_retries"),
+            "shards": [{k: s[k] for k in ("lanes", "head_lanes", "messages")} for s in e.shard_stats()]}
+
+
 def _oracle_dedup(w):
     """Oracle digests of a batch with many aliases: hash each distinct (off, len) once."""
     key = np.stack([w.off, w.len], axis=1)
@@ -693,7 +705,7 @@ def test_staged_direct_pageable(shards, monkeypatch):
             out = None if outk == "pageable" else e.pinned_empty(w.n * 32).reshape(w.n, 32)
             st0 = e.stats()
             got = e.digest_batch(w.arena, off, ln, out=out)
-            assert np.array_equal(got, exp), (meta, outk)
+            assert np.array_equal(got, exp), _mismatch(w, got, exp, e, (meta, outk))
             st1 = e.stats()
             assert st1["staged_calls"] == st0["staged_calls"] + 1 and st1["direct_calls"] == st0["direct_calls"]
             sh = e.shard_stats()
