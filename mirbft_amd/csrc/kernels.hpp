@@ -129,7 +129,19 @@ struct FoldArgs {
                               // block count and the block sum (the head's cost model needs the
                               // real longest chain, not the class's lower bound)
   uint32_t* order;            // n, kNoLane-filled -> position -> message index
-  uint32_t* info;             // out: [0] lanes, [1] head
+  uint32_t* info;             // [0] lanes, [1] positions the lane kernel skips (the head's),
+                              // [2] distinct long payloads, [3] k_fold_longs workgroups done,
+                              // [4] the early head's lanes (0: none), [5] the late head's
+                              // ([2], [3] zeroed by the caller)
+  // The early head (folding only; long_blocks 0: off): k_fold_longs claims every
+  // message of >= long_blocks blocks in the alias table before anything else,
+  // listing each distinct one in longs; when there are at most long_cap, those
+  // are the head, launched right then on the two-lane kernel over longs (info[4]),
+  // instead of after the scan and scatter, and k_fold_insert never takes a long
+  // message as fresh (so its representative is the listed one).
+  uint32_t* longs = nullptr;
+  uint32_t long_blocks = 0;
+  uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;
   // The head: the cut of the longest lanes that minimises the launch's
@@ -150,6 +162,8 @@ struct FoldArgs {
   uint32_t tiebreak = 1;         // head-bound ties go to the cut with the most lane-kernel room (A/B: 0)
 };
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st);
+// The early head's list (FoldArgs::longs), before launch_fold_plan on the same stream.
+hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st);
 // out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.
 hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st);
 

@@ -237,7 +237,9 @@ struct Device {
   // planned device calls (msha_digest_batch_device_planned): alias table,
   // representatives, bucket counters, lane order, [lanes | head]; the head of
   // long chains runs on side_stream, forked from and joined to the caller's
-  DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_info;
+  DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_info, f_longs;
+  hipStream_t head_stream = nullptr;  // a folded call's early head (FoldArgs::longs)
+  hipEvent_t ev_longs = nullptr, ev_join2 = nullptr;
   uint32_t f_epoch = 0;  // the alias table's epoch tag of the last folded call (plan.hip fold_claim)
   DevBuf probe;  // msha_clock_probe: stamps + sink
   // direct path heads (launch_head): their digests, lane-indexed; read back with
@@ -267,7 +269,7 @@ struct Device {
     gather_pool.reset();
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table, &sm_in, &sm_out, &p_meta,
                       &p_gmap, &p_devoff, &p_table, &p_slot, &p_rep, &p_cnt, &p_small, &f_table, &f_rep,
-                      &f_tmax, &f_cnt, &f_order, &f_info, &probe, &p_head})
+                      &f_tmax, &f_cnt, &f_order, &f_info, &f_longs, &probe, &p_head})
       b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
@@ -275,7 +277,8 @@ struct Device {
                       &h_head})
       b->release();
     for (hipEvent_t* e : {&ev0, &ev1, &ev_up0, &ev_up1, &ev_k0, &ev_meta, &ev_plan, &ev_p0, &ev_p1, &slot_free[0],
-                          &slot_free[1], &chunk_in, &ev_fork, &ev_fplan, &ev_join, &ev_fdone, &ev_head}) {
+                          &slot_free[1], &chunk_in, &ev_fork, &ev_fplan, &ev_join, &ev_fdone, &ev_head,
+                          &ev_longs, &ev_join2}) {
       if (*e) (void)hipEventDestroy(*e);
       *e = nullptr;
     }
@@ -285,9 +288,10 @@ struct Device {
     if (copy_stream) (void)hipStreamDestroy(copy_stream);
     if (d2h_stream) (void)hipStreamDestroy(d2h_stream);
     if (side_stream) (void)hipStreamDestroy(side_stream);
+    if (head_stream) (void)hipStreamDestroy(head_stream);
     if (ev_k) (void)hipEventDestroy(ev_k);
     ev_k = nullptr;
-    stream = copy_stream = d2h_stream = side_stream = nullptr;
+    stream = copy_stream = d2h_stream = side_stream = head_stream = nullptr;
   }
 };
 
@@ -2718,7 +2722,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     while (cap < 2 * n) cap <<= 1;
     d.f_cnt.ensure(4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets);  // counters, then FoldArgs::big
     d.f_order.ensure(4 * n);
-    d.f_info.ensure(8);
+    d.f_info.ensure(4 * 8);
     bool clear_table = false;
     if (fold) {
       // epoch-tagged slots (plan.hip fold_claim): cleared only when the table
@@ -2755,6 +2759,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     }
     if (clear_table) HIPCHK(hipMemsetAsync(d.f_table.p, 0, d.f_table.cap, ps));
     HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets, ps));
+    HIPCHK(hipMemsetAsync(d.f_info.p, 0, 4 * 8, ps));
     // (the order's positions past the last lane are filled by k_fold_scatter)
     msha::FoldArgs fa;
     fa.off = d_off;
@@ -2785,6 +2790,35 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
     fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);
+    // The early head (folded calls with a two-lane head): the distinct payloads
+    // of >= kLongBlocks blocks are listed first (k_fold_longs) and, when at most
+    // an eighth of the CUs' worth, start on the two-lane kernel on a stream of
+    // their own right then, while the alias insert, the scan and the scatter
+    // still run -- a folded storm's head no longer waits ~0.08 ms for the whole
+    // plan. MSHA_EARLY_HEAD=0: the head after the scan's cut (A/B).
+    const bool early = fold && head && two_lane && env_u64("MSHA_EARLY_HEAD", 0) != 0;
+    if (early) {
+      fa.long_blocks = (uint32_t)kLongBlocks;
+      fa.long_cap = (uint32_t)(d.cus * msha::kChain2MsgsPerWg / 8);
+      d.f_longs.ensure(4 * (uint64_t)fa.long_cap);
+      fa.longs = d.f_longs.as<uint32_t>();
+      if (!d.head_stream) HIPCHK(hipStreamCreateWithFlags(&d.head_stream, hipStreamNonBlocking));
+      for (hipEvent_t* e : {&d.ev_longs, &d.ev_join2})
+        if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+      HIPCHK(msha::launch_fold_longs(fa, d.cus, ps));
+      HIPCHK(hipEventRecord(d.ev_longs, ps));
+      HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
+      msha::LaneGate eg;
+      eg.head = fa.info + 4;
+      eg.head_part = true;
+      eg.two_lane = true;
+      msha::LaunchKind ek;
+      HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, fa.longs, nullptr, fa.long_cap, d_out,
+                                       d.err.as<uint32_t>(), d.cus, MSHA_KERNEL_COOP, d.head_stream, nullptr,
+                                       &ek, &eg));
+      count_launch(ctx, nullptr, ek);
+      HIPCHK(hipEventRecord(d.ev_join2, d.head_stream));
+    }
     HIPCHK(msha::launch_fold_plan(fa, ps));
     const uint32_t* order = d.f_order.as<uint32_t>();
     msha::LaunchKind kind;
@@ -2798,7 +2832,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       if (head) {
         HIPCHK(hipEventRecord(d.ev_fplan, d.side_stream));
         msha::LaneGate hg;
-        hg.head = fa.info + 1;
+        hg.head = fa.info + 5;  // the scan's cut (0 when the early head has the long lanes)
         hg.head_part = true;
         hg.two_lane = two_lane;
         HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, order, nullptr, fa.head_cap, d_out,
@@ -2812,6 +2846,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
                                        d.cus, ctx->kernel_policy, st, nullptr, &kind, &body));
       count_launch(ctx, nullptr, kind);
       if (head) HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
+      if (early) HIPCHK(hipStreamWaitEvent(st, d.ev_join2, 0));
     }
     if (fold) HIPCHK(msha::launch_fold_fill(fa.rep, n, d_out, st));
     HIPCHK(hipEventRecord(d.ev_fdone, st));

@@ -34,6 +34,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "kernels.hpp"
 
 namespace msha {
@@ -440,7 +442,9 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   for (uint32_t r = 0; r < kPlanItems; ++r) {
     const uint64_t i = base + r;
     if (i >= a.n) break;
-    const bool fresh = o[r] > run || (first_ever && r == 0);  // above every earlier offset
+    // above every earlier offset (a long message never: k_fold_longs claimed its key)
+    const bool fresh = (o[r] > run || (first_ever && r == 0)) &&
+                       !(a.long_blocks && dev_blocks_for(a.len[i]) >= a.long_blocks);
     if (fresh) {
       a.rep[i] = (uint32_t)i;
       fold_hist_add(hist, a.len[i]);
@@ -609,8 +613,13 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     // otherwise run as lone chains on the lane kernel (folded c5: 37 -> 128).
     const uint32_t h = best[0] == ~0ull ? 0u : part[0];
     const uint32_t hfill = (h + a.head_per_wg - 1) / a.head_per_wg * a.head_per_wg;
+    const uint32_t late = min(min(hfill, lanes), a.head_cap);
+    // an early head (k_fold_longs) is exactly the lanes of >= long_blocks blocks:
+    // the first info[4] positions of the descending order
+    const uint32_t early = a.long_blocks ? a.info[4] : 0u;
     a.info[0] = lanes;
-    a.info[1] = min(min(hfill, lanes), a.head_cap);
+    a.info[1] = early ? early : late;
+    a.info[5] = early ? 0u : late;
   }
 }
 
@@ -644,6 +653,42 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t q = a.info[0] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += stride)
     a.order[q] = kNoLane;
+}
+
+// The early head's list: every message of >= long_blocks blocks claims its
+// (off, len) in the alias table (a hot payload costs a cached read after the
+// first claim); each claimant -- one per distinct long payload -- is listed. The
+// last workgroup to finish publishes the list's length as the early head, or 0
+// when it is longer than long_cap (then the scan's cut decides, as without it).
+__global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
+    const uint64_t l = a.len[i];
+    if (dev_blocks_for(l) < a.long_blocks) continue;
+    if (fold_claim(a, i, a.off[i], l) == (uint32_t)i) {
+      const uint32_t k = atomicAdd(&a.info[2], 1u);
+      if (k < a.long_cap) a.longs[k] = (uint32_t)i;
+    }
+  }
+  __shared__ bool last;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();  // this workgroup's list entries before its count
+    last = atomicAdd(&a.info[3], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    const uint32_t c = __hip_atomic_load(&a.info[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    a.info[4] = c <= a.long_cap ? c : 0u;
+  }
+}
+
+hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
+  if (a.n == 0 || !a.long_blocks) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<uint64_t>((a.n + 255) / 256, (uint64_t)cus * 4);
+  hipLaunchKernelGGL(k_fold_longs, dim3(grid), dim3(256), 0, st, a);
+  return hipGetLastError();
 }
 
 __global__ __launch_bounds__(256) void k_fold_fill(const uint32_t* __restrict__ rep, uint64_t n,

@@ -5,6 +5,8 @@ distinct (off, len) hashed once) -- BASELINE config c5 at full size and per-rank
 slices, the head routing forced and disabled, every kernel policy, edge cases
 (one payload aliased n times, empty messages, messages past the exact block-
 count buckets) and seeded fuzz."""
+import os
+
 import numpy as np
 import pytest
 
@@ -29,6 +31,9 @@ def _expect(w, threads=16):
     uniq, first, inv = np.unique(key, axis=0, return_index=True, return_inverse=True)
     d = oracle.openssl_digest_batch(w.arena, w.off[first], w.len[first], threads)
     return d[inv.reshape(-1)]
+
+
+_EARLY = os.environ.get("MSHA_EARLY_HEAD", "0") == "1"
 
 
 def _run(engine, w, fold, stream=None):
@@ -75,7 +80,9 @@ def test_c5_rank_slice_routes_long_chains(engine, world, fold):
     after = engine.stats()
     assert np.array_equal(got, exp)
     if fold or world == 8:
-        assert _delta(before, after, "launches_coop") == 1
+        # folded: the early head (the long payloads, k_fold_longs) and the scan's
+        # cut (empty then) are two launches
+        assert _delta(before, after, "launches_coop") == (2 if fold and _EARLY else 1)
     assert _delta(before, after, "launches_lane") == 1
 
 
@@ -233,6 +240,35 @@ def test_bad_flags(engine):
     assert rc == L.MSHA_ERR_INVALID_ARG
 
 
+@pytest.mark.parametrize("early", ["0", "1"])
+def test_early_head(engine, monkeypatch, early):
+    """Folded calls with the early head (MSHA_EARLY_HEAD=1: the distinct payloads of
+    >= 256 blocks claimed and listed before the alias insert, and started on the
+    two-lane kernel right then) and without: c5 slices at 1 and 8 GPUs, a batch
+    whose long payloads are too many for the early head (it stands down and the
+    scan's cut decides), and long payloads first named by a fresh message; every
+    digest exact, the two head launches counted."""
+    monkeypatch.setenv("MSHA_EARLY_HEAD", early)
+    for world in (1, 8):
+        w = W.c5_storm(n=(1 << 23) // world // 4, first=world)
+        before = engine.stats()
+        assert np.array_equal(_run(engine, w, True), _expect(w))
+        assert _delta(before, engine.stats(), "launches_coop") == (2 if early == "1" else 1)
+    # 3,000 distinct 300-block payloads (> 256 CUs x 64 / 8): no early head
+    rng = np.random.default_rng(300)
+    n = 60_000
+    ln = np.full(n, 512, np.uint64)
+    longs = rng.choice(n, 3000, replace=False)
+    ln[longs] = 300 * 64 - 20
+    off = np.concatenate([[0], np.cumsum((ln + np.uint64(15)) // np.uint64(16) * np.uint64(16))[:-1]]).astype(np.uint64)
+    # every long payload named again by a later message (aliases of fresh ones)
+    alias = rng.choice(n, 3000, replace=False)
+    off[alias], ln[alias] = off[longs], ln[longs]
+    arena = W.random_bytes(W.SEED ^ 0x300, 0, int(off.max() + ln.max()) + 64)
+    w = W.Workload("many-longs", arena, off, ln)
+    assert np.array_equal(_run(engine, w, True), _expect(w))
+
+
 def test_big_bucket_messages_head(engine, monkeypatch):
     """Messages of 4,096 blocks or more share power-of-two block-count classes;
     the planner's head cost model reads each class's real longest chain and
@@ -253,7 +289,9 @@ def test_big_bucket_messages_head(engine, monkeypatch):
         for fold in (False, True):
             before = engine.stats()
             assert np.array_equal(_run(engine, w, fold), exp)
-            assert _delta(before, engine.stats(), "launches_coop") == 1   # the long chains got a head
+            # the long chains got a head (folded on the two-lane kernel: the early
+            # head and the scan's cut, two launches)
+            assert _delta(before, engine.stats(), "launches_coop") == (2 if fold and chain2 == "2" and _EARLY else 1)
 
 
 def test_graph_capture_refused_cleanly(engine):
