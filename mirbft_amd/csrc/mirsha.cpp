@@ -2796,7 +2796,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // their own right then, while the alias insert, the scan and the scatter
     // still run -- a folded storm's head no longer waits ~0.08 ms for the whole
     // plan. MSHA_EARLY_HEAD=0: the head after the scan's cut (A/B).
-    const bool early = fold && head && two_lane && env_u64("MSHA_EARLY_HEAD", 0) != 0;
+    const bool early = fold && head && two_lane && env_u64("MSHA_EARLY_HEAD", 1) != 0;
     if (early) {
       fa.long_blocks = (uint32_t)kLongBlocks;
       fa.long_cap = (uint32_t)(d.cus * msha::kChain2MsgsPerWg / 8);

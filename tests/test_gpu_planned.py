@@ -33,7 +33,7 @@ def _expect(w, threads=16):
     return d[inv.reshape(-1)]
 
 
-_EARLY = os.environ.get("MSHA_EARLY_HEAD", "0") == "1"
+_EARLY = os.environ.get("MSHA_EARLY_HEAD", "1") == "1"
 
 
 def _run(engine, w, fold, stream=None):
