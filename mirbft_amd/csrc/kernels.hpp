@@ -131,8 +131,9 @@ struct FoldArgs {
   uint32_t* order;            // n, kNoLane-filled -> position -> message index
   uint32_t* info;             // [0] lanes, [1] positions the lane kernel skips (the head's),
                               // [2] distinct long payloads, [3] k_fold_longs workgroups done,
-                              // [4] the early head's lanes (0: none), [5] the late head's
-                              // ([2], [3] zeroed by the caller)
+                              // [4] the early head's lanes (0: none), [5] the late head's,
+                              // [8..11] two u64: the batch's blocks and longest chain
+                              // ([2], [3], [8..11] zeroed by the caller: 12 words)
   // The early head (folding only; long_blocks 0: off): k_fold_longs claims every
   // message of >= long_blocks blocks in the alias table before anything else,
   // listing each distinct one in longs; when there are at most long_cap, those
@@ -161,8 +162,10 @@ struct FoldArgs {
   uint32_t head_per_wg = 128;    // messages per head workgroup (one CU each)
   uint32_t tiebreak = 1;         // head-bound ties go to the cut with the most lane-kernel room (A/B: 0)
 };
-hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st);
-// The early head's list (FoldArgs::longs), before launch_fold_plan on the same stream.
+// scan_after (may be null): an event k_fold_scan waits for (the early head's list).
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_after = nullptr);
+// The early head's list (FoldArgs::longs): on a stream of its own, beside the alias
+// insert (both claim through the same table); the scan waits for it.
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st);
 // out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.
 hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st);

@@ -2722,7 +2722,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     while (cap < 2 * n) cap <<= 1;
     d.f_cnt.ensure(4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets);  // counters, then FoldArgs::big
     d.f_order.ensure(4 * n);
-    d.f_info.ensure(4 * 8);
+    d.f_info.ensure(4 * 12);
     bool clear_table = false;
     if (fold) {
       // epoch-tagged slots (plan.hip fold_claim): cleared only when the table
@@ -2759,7 +2759,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     }
     if (clear_table) HIPCHK(hipMemsetAsync(d.f_table.p, 0, d.f_table.cap, ps));
     HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets, ps));
-    HIPCHK(hipMemsetAsync(d.f_info.p, 0, 4 * 8, ps));
+    HIPCHK(hipMemsetAsync(d.f_info.p, 0, 4 * 12, ps));
     // (the order's positions past the last lane are filled by k_fold_scatter)
     msha::FoldArgs fa;
     fa.off = d_off;
@@ -2791,11 +2791,11 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
     fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);
     // The early head (folded calls with a two-lane head): the distinct payloads
-    // of >= kLongBlocks blocks are listed first (k_fold_longs) and, when at most
-    // an eighth of the CUs' worth, start on the two-lane kernel on a stream of
-    // their own right then, while the alias insert, the scan and the scatter
-    // still run -- a folded storm's head no longer waits ~0.08 ms for the whole
-    // plan. MSHA_EARLY_HEAD=0: the head after the scan's cut (A/B).
+    // of >= kLongBlocks blocks are listed (k_fold_longs, beside the alias insert)
+    // and, when at most an eighth of the CUs' worth, start on the two-lane kernel
+    // on a stream of their own right then, while the insert, the scan and the
+    // scatter still run -- a folded storm's head no longer waits ~0.08 ms for the
+    // whole plan. MSHA_EARLY_HEAD=0: the head after the scan's cut (A/B).
     const bool early = fold && head && two_lane && env_u64("MSHA_EARLY_HEAD", 1) != 0;
     if (early) {
       fa.long_blocks = (uint32_t)kLongBlocks;
@@ -2805,9 +2805,12 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       if (!d.head_stream) HIPCHK(hipStreamCreateWithFlags(&d.head_stream, hipStreamNonBlocking));
       for (hipEvent_t* e : {&d.ev_longs, &d.ev_join2})
         if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-      HIPCHK(msha::launch_fold_longs(fa, d.cus, ps));
+      // the list on the head's stream, forked after the planner's memsets: it
+      // runs beside the tile scans and the alias insert, not in front of them
       HIPCHK(hipEventRecord(d.ev_longs, ps));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
+      HIPCHK(msha::launch_fold_longs(fa, d.cus, d.head_stream));
+      HIPCHK(hipEventRecord(d.ev_longs, d.head_stream));
       msha::LaneGate eg;
       eg.head = fa.info + 4;
       eg.head_part = true;
@@ -2819,7 +2822,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       count_launch(ctx, nullptr, ek);
       HIPCHK(hipEventRecord(d.ev_join2, d.head_stream));
     }
-    HIPCHK(msha::launch_fold_plan(fa, ps));
+    HIPCHK(msha::launch_fold_plan(fa, ps, early ? d.ev_longs : nullptr));
     const uint32_t* order = d.f_order.as<uint32_t>();
     msha::LaunchKind kind;
     if (all_coop) {

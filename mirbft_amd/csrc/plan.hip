@@ -657,30 +657,57 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
 
 // The early head's list: every message of >= long_blocks blocks claims its
 // (off, len) in the alias table (a hot payload costs a cached read after the
-// first claim); each claimant -- one per distinct long payload -- is listed. The
+// first claim); each claimant -- one per distinct long payload -- is listed. It
+// runs beside k_fold_insert: whichever claims a key first, both read the same
+// claimant back, and the claimant, a long message itself, lists itself here. The
 // last workgroup to finish publishes the list's length as the early head, or 0
 // when it is longer than long_cap (then the scan's cut decides, as without it).
+// It also estimates the lane kernel's share -- every short message's blocks (a
+// storm's re-hashes are its long payloads; short ones are mostly distinct) --
+// and finds the longest chain: when that share would keep the lane kernel busy
+// past the head's chain anyway (c5 on one GPU: ~60 M blocks against one
+// 1,427-block chain), starting the head early buys nothing and its list only
+// competes with the insert for the table, so the head then stands down too.
 __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t sum = 0, mx = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
     const uint64_t l = a.len[i];
-    if (dev_blocks_for(l) < a.long_blocks) continue;
+    const uint64_t blocks = dev_blocks_for(l);
+    mx = max(mx, blocks);
+    if (blocks < a.long_blocks) {
+      sum += blocks;
+      continue;
+    }
     if (fold_claim(a, i, a.off[i], l) == (uint32_t)i) {
+      sum += blocks;
       const uint32_t k = atomicAdd(&a.info[2], 1u);
       if (k < a.long_cap) a.longs[k] = (uint32_t)i;
     }
   }
+  __shared__ unsigned long long s_sum, s_max;
   __shared__ bool last;
+  if (threadIdx.x == 0) s_sum = s_max = 0;
   __syncthreads();
+  atomicAdd(&s_sum, (unsigned long long)sum);
+  atomicMax(&s_max, (unsigned long long)mx);
+  __syncthreads();
+  unsigned long long* g = reinterpret_cast<unsigned long long*>(a.info + 8);  // [blocks, longest]
   if (threadIdx.x == 0) {
-    __threadfence();  // this workgroup's list entries before its count
+    atomicAdd(&g[0], s_sum);
+    atomicMax(&g[1], s_max);
+    __threadfence();  // this workgroup's list entries and sums before its count
     last = atomicAdd(&a.info[3], 1u) == gridDim.x - 1;
   }
   __syncthreads();
   if (last && threadIdx.x == 0) {
     __threadfence();
     const uint32_t c = __hip_atomic_load(&a.info[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    a.info[4] = c <= a.long_cap ? c : 0u;
+    const uint64_t tot = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t lng = __hip_atomic_load(&g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t_body = tot * a.wave_block_cycles / (64ull * a.simds);
+    const uint64_t t_head = lng * a.coop_cycles;
+    a.info[4] = c <= a.long_cap && t_body < t_head ? c : 0u;
   }
 }
 
@@ -703,7 +730,7 @@ __global__ __launch_bounds__(256) void k_fold_fill(const uint32_t* __restrict__ 
   dst[1] = src[1];
 }
 
-hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st) {
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_after) {
   if (a.n == 0) return hipSuccess;
   const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
   if (a.table) {
@@ -713,6 +740,10 @@ hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st) {
   }
   const unsigned ftiles = (unsigned)((a.n + kFoldTile - 1) / kFoldTile);
   if (!a.table) hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
+  if (scan_after) {
+    const hipError_t e = hipStreamWaitEvent(st, scan_after, 0);
+    if (e != hipSuccess) return e;
+  }
   hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(k_fold_scatter, dim3(ftiles), dim3(256), 0, st, a);
   return hipGetLastError();

@@ -22,7 +22,7 @@ hipError_t launch_digest_batch(const uint8_t*, const uint64_t*, const uint64_t*,
                                const SplitPlan*, LaunchKind*, const LaneGate*) {
   return hipErrorNotSupported;
 }
-hipError_t launch_fold_plan(const FoldArgs&, hipStream_t) { return hipErrorNotSupported; }
+hipError_t launch_fold_plan(const FoldArgs&, hipStream_t, hipEvent_t) { return hipErrorNotSupported; }
 hipError_t launch_fold_longs(const FoldArgs&, int, hipStream_t) { return hipErrorNotSupported; }
 hipError_t launch_fold_fill(const uint32_t*, uint64_t, uint8_t*, hipStream_t) { return hipErrorNotSupported; }
 hipError_t launch_clock_probe(uint32_t, uint32_t, uint64_t*, uint32_t*, hipStream_t) { return hipErrorNotSupported; }
