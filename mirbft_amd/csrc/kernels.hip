@@ -938,6 +938,10 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
 #ifndef MSHA_CHAIN2_FORM
 #define MSHA_CHAIN2_FORM 4
 #endif
+#ifndef MSHA_CHAIN2_PAIR
+#define MSHA_CHAIN2_PAIR 1
+#endif
+constexpr uint32_t kC2Per = MSHA_CHAIN2_PAIR ? 2 : 1;  // blocks per producer/consumer barrier
 #define MSHA_ASM_SIGMA(X)                                                                        \
   "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh1]\n\t"                                       \
   "v_alignbit_b32 %[s2], %[" #X "], %[" #X "], %[sh2]\n\t"                                       \
@@ -995,7 +999,7 @@ constexpr int kC2Quads = 8;  // K+W quads a consumer lane reads per block
 #define MSHA_DQ(cur, nxt, q)                                                                     \
   {                                                                                              \
     const uint4 v_ = cur[q];                                                                     \
-    nxt[q] = kw[ns][col + (q) * qstride];                                                        \
+    nxt[q] = nk[col + (q) * qstride];                                                            \
     uint32_t s1_, s2_, s3_, s_, sk_, c_, u_, m_, t_, y_;                                         \
     asm volatile(MSHA_ASM_EROUND(X, Y, Z, W, k0) MSHA_ASM_AROUND(W, X, Y, Z, k0)                 \
                  MSHA_ASM_EROUND(Z, W, X, Y, k1) MSHA_ASM_AROUND(Y, Z, W, X, k1)                 \
@@ -1008,7 +1012,7 @@ constexpr int kC2Quads = 16;
 #define MSHA_DQ(cur, nxt, q)                                                                     \
   {                                                                                              \
     const uint4 v_ = cur[q];                                                                     \
-    nxt[q] = kw[ns][col + (q) * qstride];                                                        \
+    nxt[q] = nk[col + (q) * qstride];                                                            \
     uint32_t s1_, s2_, s3_, s_, sk_, c_, u_, m_, t_, y_;                                         \
     asm volatile(MSHA_ASM_ROUND3(X, Y, Z, W, k0) MSHA_ASM_ROUND3(W, X, Y, Z, k1)                 \
                  MSHA_ASM_ROUND3(Z, W, X, Y, k2) MSHA_ASM_ROUND3(Y, Z, W, X, k3)                 \
@@ -1017,7 +1021,7 @@ constexpr int kC2Quads = 16;
   }
 #endif
 // One block b from cur (read during the previous block), reading block b+1's
-// K+W (slot ns) into nxt; the digest is stored after the message's last block.
+// K+W (its LDS slot nk) into nxt; the digest is stored after the message's last block.
 #define MSHA_DBLOCK(cur, nxt)                                                                    \
   {                                                                                              \
     uint32_t X = H0, Y = H1, Z = H2, W = H3;                                                     \
@@ -1061,7 +1065,7 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
                                                        uint32_t* __restrict__ err,
                                                        const uint32_t* __restrict__ limit) {
   // [slot][quad t/4][message] x 16 B, then 16 zero quads (the a-lanes' K+W)
-  __shared__ uint4 kw[2][kCoopSlotQuads * 64 + kCoopSlotQuads];
+  __shared__ uint4 kw[2][kC2Per][kCoopSlotQuads * 64 + kCoopSlotQuads];
   __shared__ uint32_t s_nb;
   if (EXCL) asm volatile("" ::: "v255", "a255");  // exclusive CU (see k_digest_coop EXCL)
   if (EXCL) __builtin_amdgcn_s_setprio(3);
@@ -1097,8 +1101,9 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
   const uint32_t nb = nfull + (r < 56 ? 1 : 2);
   if (threadIdx.x == 0) s_nb = 0;
-  if (MSHA_CHAIN2_FORM == 3 && threadIdx.x < 2 * kCoopSlotQuads)  // form 3: the a-lanes' zero quads
-    kw[threadIdx.x >> 4][kCoopSlotQuads * 64 + (threadIdx.x & 15)] = make_uint4(0, 0, 0, 0);
+  if (MSHA_CHAIN2_FORM == 3 && threadIdx.x < 2 * kC2Per * kCoopSlotQuads)  // form 3: the a-lanes' zero quads
+    kw[threadIdx.x / (kC2Per * 16)][(threadIdx.x >> 4) % kC2Per][kCoopSlotQuads * 64 + (threadIdx.x & 15)] =
+        make_uint4(0, 0, 0, 0);
   __syncthreads();
   if (producer && active) atomicMax(&s_nb, nb);
   __syncthreads();
@@ -1117,13 +1122,15 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
         length_block(L, w);
       }
       if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
+      uint4* slot = &kw[(b / kC2Per) & 1][b % kC2Per][lane];
       if (MSHA_CHAIN2_FORM == 4)
-        schedule_kw_eo(w, &kw[b & 1][lane]);
+        schedule_kw_eo(w, slot);
       else
-        schedule_kw(w, &kw[b & 1][lane]);
-      MSHA_C2_BARRIER(b)  // barrier b: slot b & 1 holds block b
+        schedule_kw(w, slot);
+      // barrier g: slot g & 1 holds group g (kC2Per blocks)
+      if (b % kC2Per == kC2Per - 1 || b + 1 == NB) MSHA_C2_BARRIER(b / kC2Per)
     }
-    MSHA_C2_BARRIER(NB)  // barrier NB: the consumers' last (they wait one block ahead)
+    MSHA_C2_BARRIER((NB + kC2Per - 1) / kC2Per)  // the consumers' last (they wait one group ahead)
   } else {
     // e-side: e f g h, rotates 6 11 25; a-side: a b c d, rotates 2 13 22
     uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
@@ -1143,19 +1150,58 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     // waits for every outstanding LDS read) -- while block b computes. Two
     // register sets alternate by unrolling the block loop twice, so nothing is
     // copied between blocks.
+    // MSHA_CHAIN2_PAIR: a barrier per PAIR of blocks -- the producer schedules
+    // two blocks into a slot, the consumers hold four register sets (the pair
+    // they compute, the pair they read) -- halving the barriers a chain pays.
+#if MSHA_CHAIN2_PAIR
+    uint4 ka[kC2Quads], kb[kC2Quads], kc[kC2Quads], kd[kC2Quads];
+    MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds blocks 0 and 1
+#pragma unroll
+    for (int q = 0; q < kC2Quads; ++q) {
+      ka[q] = kw[0][0][col + q * qstride];
+      kb[q] = kw[0][1][col + q * qstride];
+    }
+    const uint32_t NP = (NB + 1) / 2;
+    for (uint32_t g = 0; g < NP; ++g) {
+      MSHA_C2_BARRIER(g + 1)  // reads past the last block are harmless (unused)
+      {
+        const uint32_t b = 2 * g;
+        const uint4* nk = kw[(g + 1) & 1][0];
+        MSHA_DBLOCK(ka, kc)
+      }
+      {
+        const uint32_t b = 2 * g + 1;
+        const uint4* nk = kw[(g + 1) & 1][1];
+        MSHA_DBLOCK(kb, kd)
+      }
+      if (++g == NP) break;
+      MSHA_C2_BARRIER(g + 1)
+      {
+        const uint32_t b = 2 * g;
+        const uint4* nk = kw[(g + 1) & 1][0];
+        MSHA_DBLOCK(kc, ka)
+      }
+      {
+        const uint32_t b = 2 * g + 1;
+        const uint4* nk = kw[(g + 1) & 1][1];
+        MSHA_DBLOCK(kd, kb)
+      }
+    }
+#else
     uint4 ka[kC2Quads], kb[kC2Quads];
     MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds block 0
 #pragma unroll
-    for (int q = 0; q < kC2Quads; ++q) ka[q] = kw[0][col + q * qstride];
+    for (int q = 0; q < kC2Quads; ++q) ka[q] = kw[0][0][col + q * qstride];
     for (uint32_t b = 0; b < NB; ++b) {
       MSHA_C2_BARRIER(b + 1)
-      unsigned ns = (b + 1) & 1;  // a read past the last block is harmless (unused)
+      const uint4* nk = kw[(b + 1) & 1][0];  // a read past the last block is harmless (unused)
       MSHA_DBLOCK(ka, kb)
       if (++b == NB) break;
       MSHA_C2_BARRIER(b + 1)
-      ns = (b + 1) & 1;
+      nk = kw[(b + 1) & 1][0];
       MSHA_DBLOCK(kb, ka)
     }
+#endif
   }
 }
 #undef MSHA_DBLOCK
