@@ -941,7 +941,12 @@ __global__ __launch_bounds__(256) void k_digest_coop(const uint8_t* __restrict__
 #ifndef MSHA_CHAIN2_PAIR
 #define MSHA_CHAIN2_PAIR 1
 #endif
-constexpr uint32_t kC2Per = MSHA_CHAIN2_PAIR ? 2 : 1;  // blocks per producer/consumer barrier
+constexpr uint32_t kC2Per = MSHA_CHAIN2_PAIR ? 2 : 1;  // LDS slots' blocks (the most per barrier)
+// A workgroup pairs blocks per barrier only when its longest message has at
+// least this many: pairing delays the consumers' first block by two producer
+// blocks, which a short chain pays in full (1,024 x 640 B: 22.3 -> 25.5 us)
+// while a long one gains (256 x 64 KiB: 1.420 -> 1.405 ms; tools/ab_lib.sh).
+constexpr uint32_t kC2PairMinBlocks = 64;
 #define MSHA_ASM_SIGMA(X)                                                                        \
   "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh1]\n\t"                                       \
   "v_alignbit_b32 %[s2], %[" #X "], %[" #X "], %[sh2]\n\t"                                       \
@@ -1108,6 +1113,7 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   if (producer && active) atomicMax(&s_nb, nb);
   __syncthreads();
   const uint32_t NB = s_nb;
+  const uint32_t per = kC2Per == 2 && NB >= kC2PairMinBlocks ? 2u : 1u;  // blocks per barrier
   if (producer) {
     uint32_t raw[16], w[16];
     if (active) load_block16<MODE>(pa, raw);
@@ -1122,15 +1128,15 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
         length_block(L, w);
       }
       if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
-      uint4* slot = &kw[(b / kC2Per) & 1][b % kC2Per][lane];
+      uint4* slot = &kw[(b / per) & 1][b % per][lane];
       if (MSHA_CHAIN2_FORM == 4)
         schedule_kw_eo(w, slot);
       else
         schedule_kw(w, slot);
-      // barrier g: slot g & 1 holds group g (kC2Per blocks)
-      if (b % kC2Per == kC2Per - 1 || b + 1 == NB) MSHA_C2_BARRIER(b / kC2Per)
+      // barrier g: slot g & 1 holds group g (per blocks)
+      if (b % per == per - 1 || b + 1 == NB) MSHA_C2_BARRIER(b / per)
     }
-    MSHA_C2_BARRIER((NB + kC2Per - 1) / kC2Per)  // the consumers' last (they wait one group ahead)
+    MSHA_C2_BARRIER((NB + per - 1) / per)  // the consumers' last (they wait one group ahead)
   } else {
     // e-side: e f g h, rotates 6 11 25; a-side: a b c d, rotates 2 13 22
     uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
@@ -1154,6 +1160,7 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     // two blocks into a slot, the consumers hold four register sets (the pair
     // they compute, the pair they read) -- halving the barriers a chain pays.
 #if MSHA_CHAIN2_PAIR
+    if (per == 2) {
     uint4 ka[kC2Quads], kb[kC2Quads], kc[kC2Quads], kd[kC2Quads];
     MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds blocks 0 and 1
 #pragma unroll
@@ -1187,7 +1194,9 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
         MSHA_DBLOCK(kd, kb)
       }
     }
-#else
+    return;
+    }
+#endif
     uint4 ka[kC2Quads], kb[kC2Quads];
     MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds block 0
 #pragma unroll
@@ -1201,7 +1210,6 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
       nk = kw[(b + 1) & 1][0];
       MSHA_DBLOCK(kb, ka)
     }
-#endif
   }
 }
 #undef MSHA_DBLOCK
