@@ -270,7 +270,8 @@ func partsEqual(a, b [][]byte) bool {
 // so a pointer seen before is the same payload; acks deserialized from the
 // network hold equal copies, found by comparing the bytes of earlier payloads
 // from the same origin node with the same length (a byzantine copy that differs
-// is packed and hashed on its own). alias[i] = that earlier action, or -1.
+// is packed and hashed on its own). A pointer hit whose Data differs in length
+// falls back to that byte compare. alias[i] = that earlier action, or -1.
 func epochChangeAliases(reqs []*state.ActionHashRequest) (alias []int, size int) {
 	type contentKey struct {
 		origin uint64
@@ -288,7 +289,10 @@ func epochChangeAliases(reqs []*state.ActionHashRequest) (alias []int, size int)
 				byPtr = map[*msgs.EpochChange]int{}
 				byContent = map[contentKey][]int{}
 			}
-			if j, seen := byPtr[ec.EpochChange]; seen && ec.EpochChange != nil {
+			// a pointer seen before names the same payload only if the Data built
+			// from it has the same length (the drop-in's contract is SHA-256(Data):
+			// Data built differently from a shared message is compared byte for byte)
+			if j, seen := byPtr[ec.EpochChange]; seen && ec.EpochChange != nil && partsLen(reqs[j].Data) == l {
 				alias[i] = j
 				continue
 			}

@@ -277,9 +277,16 @@ inline std::vector<int64_t> EpochChangeAliases(const std::vector<const ActionHas
     const auto* o = reqs[i]->origin ? std::get_if<HashOriginEpochChange>(&reqs[i]->origin->type) : nullptr;
     if (!o) continue;
     const void* key = o->epoch_change.get();
+    auto parts_len = [](const std::vector<Bytes>& parts) {
+      size_t n = 0;
+      for (auto& p : parts) n += p.size();
+      return n;
+    };
     if (key) {
+      // the same message names the same payload only if the Data built from it
+      // has the same length (the contract is SHA-256(Data)); else compare bytes
       auto it = by_obj.find(key);
-      if (it != by_obj.end()) {
+      if (it != by_obj.end() && parts_len(reqs[it->second]->data) == parts_len(reqs[i]->data)) {
         alias[i] = it->second;
         continue;
       }

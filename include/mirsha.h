@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 8u
+#define MSHA_ABI_VERSION 9u
 
 enum {
   MSHA_OK = 0,
@@ -120,6 +120,13 @@ typedef struct {
 } msha_shard_stats;
 
 uint32_t msha_abi_version(void);
+
+/* The build this library is: "src=<16 hex>;flags=<compile flags>", where src is
+ * a hash of the sources it was compiled from (mirbft_amd/csrc/Makefile). A test
+ * log names the build it ran with it; tests/conftest.py refuses a GPU session
+ * whose library is not the tree's own (an experiment's build left in place).
+ * Diagnostic, no reference counterpart (ABI 9). */
+const char* msha_build_id(void);
 
 /* Number of visible HIP devices (0 when none). */
 int msha_device_count(int* n);

@@ -14,7 +14,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmirsha.so")
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -94,6 +94,7 @@ class MshaClockInfo(ctypes.Structure):
 # name -> (restype, argtypes)
 SIGNATURES = {
     "msha_abi_version": (ctypes.c_uint32, []),
+    "msha_build_id": (ctypes.c_char_p, []),
     "msha_device_count": (ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     "msha_ctx_create": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_ctxp)]),
     "msha_ctx_create_err": (ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_ctxp), ctypes.c_char_p,
@@ -169,3 +170,29 @@ def lib() -> ctypes.CDLL:
         raise ImportError("libmirsha ABI version mismatch")
     _lib = L
     return L
+
+
+# The files msha_build_id()'s src hash covers, in the Makefile's order (SRCS).
+_SRC_FILES = ("sha256_device.hpp", "kernels.hpp", "kernels.hip", "plan.hip", "mirsha.cpp",
+              os.path.join("..", "..", "include", "mirsha.h"))
+
+
+def source_id() -> str:
+    """The src hash of the tree's sources, as the Makefile computes it for msha_build_id()."""
+    import hashlib
+    h = hashlib.sha256()
+    for f in _SRC_FILES:
+        with open(os.path.join(_HERE, "csrc", f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_id() -> dict:
+    """The loaded library's build: its src hash and flags, and whether it is the tree's own
+    build (src equal to source_id() and no experiment's -D overrides in the flags)."""
+    raw = lib().msha_build_id().decode()
+    fields = dict(kv.split("=", 1) for kv in raw.split(";"))
+    src, flags = fields.get("src", ""), fields.get("flags", "")
+    tree = source_id()
+    return {"id": raw, "src": src, "flags": flags, "tree_src": tree,
+            "matches_tree": src == tree and not any(t.startswith("-D") for t in flags.split())}

@@ -1069,8 +1069,10 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
                                                        uint64_t n, uint8_t* __restrict__ out,
                                                        uint32_t* __restrict__ err,
                                                        const uint32_t* __restrict__ limit) {
-  // [slot][quad t/4][message] x 16 B, then 16 zero quads (the a-lanes' K+W)
-  __shared__ uint4 kw[2][kC2Per][kCoopSlotQuads * 64 + kCoopSlotQuads];
+  // [slot][quad t/4][message] x 16 B, then (form 3 only) 16 zero quads, the
+  // a-lanes' K+W. 2 x 2 x 16 KiB = 64 KiB with pairing: two workgroups a CU at
+  // most (a head launch, EXCL, runs one a CU anyway).
+  __shared__ uint4 kw[2][kC2Per][kCoopSlotQuads * 64 + (MSHA_CHAIN2_FORM == 3 ? kCoopSlotQuads : 0)];
   __shared__ uint32_t s_nb;
   if (EXCL) asm volatile("" ::: "v255", "a255");  // exclusive CU (see k_digest_coop EXCL)
   if (EXCL) __builtin_amdgcn_s_setprio(3);
@@ -1106,9 +1108,11 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
   const uint32_t nb = nfull + (r < 56 ? 1 : 2);
   if (threadIdx.x == 0) s_nb = 0;
-  if (MSHA_CHAIN2_FORM == 3 && threadIdx.x < 2 * kC2Per * kCoopSlotQuads)  // form 3: the a-lanes' zero quads
+#if MSHA_CHAIN2_FORM == 3
+  if (threadIdx.x < 2 * kC2Per * kCoopSlotQuads)  // form 3: the a-lanes' zero quads
     kw[threadIdx.x / (kC2Per * 16)][(threadIdx.x >> 4) % kC2Per][kCoopSlotQuads * 64 + (threadIdx.x & 15)] =
         make_uint4(0, 0, 0, 0);
+#endif
   __syncthreads();
   if (producer && active) atomicMax(&s_nb, nb);
   __syncthreads();

@@ -88,6 +88,7 @@ struct PlanArgs {
   uint32_t* slot;         // m: each message's table slot (with table)
   uint32_t* rep;          // out, m: the first message with the same (off, len)
   uint64_t pieces = 1;    // upload pieces of the shard
+  uint32_t piece_shift = kDirectChunkShift;  // a piece is 2^piece_shift device bytes
   // Lane groups: one per (region, piece), region 0 = long chains (blocks >=
   // long_blocks; long_blocks 0: no such region), region 1 = the rest; group
   // g = region * pieces + piece, chunks = the number of groups.

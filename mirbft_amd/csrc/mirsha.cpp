@@ -1188,10 +1188,12 @@ void launch_lanes(msha_ctx* ctx, Device& d, Plan& P, size_t c, bool last, double
 
 // Long chains on the direct path: a payload of at least kLongBlocks blocks
 // (16 KiB: ~0.8 ms as a chain on the lane kernel, more than an upload piece
-// takes to land) when the batch has one; MSHA_HOST_HEAD=0 disables (A/B).
+// takes to land) when the batch has one; MSHA_HOST_HEAD=0 disables (A/B). A
+// context held to the lane kernel (MSHA_KERNEL_LANE) runs no heads, as the
+// device-planned path does not: its long payloads stay ordinary lanes.
 constexpr uint64_t kLongBlocks = 256;
-uint64_t long_chain_blocks(uint64_t bmax) {
-  if (env_u64("MSHA_HOST_HEAD", 1) == 0) return 0;
+uint64_t long_chain_blocks(uint64_t bmax, uint32_t policy) {
+  if (env_u64("MSHA_HOST_HEAD", 1) == 0 || policy == MSHA_KERNEL_LANE) return 0;
   return bmax >= kLongBlocks ? kLongBlocks : 0;
 }
 // At most this many long lanes run as heads (two-lane chains, 64 per CU): half
@@ -1729,7 +1731,7 @@ uint64_t build_gmap(const std::vector<uint8_t>& mark, uint64_t gbase, uint64_t n
 // build_gmap), split where device offsets cross a kDirectChunk boundary.
 template <class F>
 void for_each_upload(const uint64_t* gmap, const std::vector<uint8_t>& mark, uint64_t ng, uint64_t gbase,
-                     uint64_t glo, unsigned gs, uint64_t lo, uint64_t hi, F&& f) {
+                     uint64_t glo, unsigned gs, uint64_t lo, uint64_t hi, F&& f, uint64_t piece_bytes = kDirectChunk) {
   const uint64_t G = 1ull << gs;
   for (int cls = 0; cls < 2; ++cls) {
     auto in_cls = [&](uint64_t g) {
@@ -1746,7 +1748,7 @@ void for_each_upload(const uint64_t* gmap, const std::vector<uint8_t>& mark, uin
       for (uint64_t pos = h0; pos < h1;) {
         const uint64_t r = pos - glo;
         const uint64_t dev = gmap[(r >> gs) - gbase] + (r & (G - 1));
-        const uint64_t piece = std::min(h1 - pos, (dev / kDirectChunk + 1) * kDirectChunk - dev);
+        const uint64_t piece = std::min(h1 - pos, (dev / piece_bytes + 1) * piece_bytes - dev);
         f(pos, dev, piece);
         pos += piece;
       }
@@ -1917,6 +1919,19 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
                 const uint8_t* arena, uint8_t* out, const BatchScan& sc, EarlyMeta* early, bool staged) {
   const uint32_t k = (uint32_t)ctx->devs.size();
   const bool out_pinned = is_pinned_host(out) && is_pinned_host(out + 32 * n - 1);
+  // Interleaving knobs (tests, read per call): upload pieces of 2^MSHA_DIRECT_PIECE_SHIFT
+  // device bytes (16..26; 26 = 64 MiB, the default) and, on the staged path,
+  // staging slots of MSHA_STAGED_SLOT_BYTES (64 KiB .. 32 MiB, the default) with
+  // a pause of MSHA_STAGED_DELAY_US before each refill. Small pieces and slots
+  // and a pause make the plan arrive, and heads and lane groups launch, between
+  // slot refills while later pieces still upload (tests/test_gpu_parity.py
+  // test_staged_direct_interleaved).
+  const unsigned piece_shift =
+      (unsigned)std::min<uint64_t>(msha::kDirectChunkShift, std::max<uint64_t>(16, env_u64("MSHA_DIRECT_PIECE_SHIFT", msha::kDirectChunkShift)));
+  const uint64_t piece_bytes = 1ull << piece_shift;
+  const uint64_t slot_bytes =
+      std::min<uint64_t>(kChunkBytes, std::max<uint64_t>(64 << 10, env_u64("MSHA_STAGED_SLOT_BYTES", kChunkBytes))) & ~uint64_t(63);
+  const uint64_t slot_delay_us = std::min<uint64_t>(env_u64("MSHA_STAGED_DELAY_US", 0), 100000);
   // off/len in pinned memory (msha_pinned_alloc, as the Go adapter packs them):
   // uploaded as they are, no staging copy (one shard: already on the way, EarlyMeta)
   const bool meta_early = early && early->queued();
@@ -1983,7 +1998,7 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
     mark.assign(nG, 0);
     // Long chains (>= kLongBlocks blocks) get their payloads uploaded first and,
     // when few enough, a head launch of their own (below).
-    const uint64_t long_blocks = long_chain_blocks(sc.bmax);
+    const uint64_t long_blocks = long_chain_blocks(sc.bmax, ctx->kernel_policy);
     const ShardSpan sh = stage_and_mark(O, L, m, glo, gs, h_off, h_len, mark, long_blocks);
     const bool any = sh.any();                       // some payload byte at all
     const uint64_t gbase = any ? sh.g0 : 0, ng = any ? sh.g1 - sh.g0 + 1 : 1;
@@ -1993,7 +2008,7 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
     d.arena_bytes = dev_bytes;
     trace("staged + marked", s, t0);
     // 2. uploads: metadata + granule map first (the planner needs them)
-    const uint64_t pieces = std::max<uint64_t>(1, (dev_bytes + kDirectChunk - 1) / kDirectChunk);
+    const uint64_t pieces = std::max<uint64_t>(1, (dev_bytes + piece_bytes - 1) / piece_bytes);
     const uint64_t chunks = long_blocks ? 2 * pieces : pieces;  // lane groups: (region, piece)
     d.arena.ensure(dev_bytes + msha::kArenaSlack);
     d.p_gmap.ensure(8 * ng);
@@ -2058,6 +2073,7 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
     pa.slot = aliases ? d.p_slot.as<uint32_t>() : nullptr;
     pa.rep = d.p_rep.as<uint32_t>();
     pa.pieces = pieces;
+    pa.piece_shift = piece_shift;
     pa.long_blocks = long_blocks;
     pa.chunks = chunks;
     pa.B = B;
@@ -2139,10 +2155,10 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
         launch_lanes(ctx, d, P, next_group, next_group + 1 == groups, t0, out, out_pinned);
       }
     };
-    // event c once every byte below device offset (c+1)*kDirectChunk is queued
+    // event c once every byte below device offset (c+1)*piece_bytes is queued
     uint64_t c = 0, uploaded = 0;
     auto pieces_done = [&](uint64_t dev_end) {
-      for (; c < pieces && (c + 1) * kDirectChunk <= dev_end; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
+      for (; c < pieces && (c + 1) * piece_bytes <= dev_end; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
     };
     unsigned slot_i = 0;
     if (staged) {  // two pinned staging slots, refilled as their H2D drains
@@ -2164,9 +2180,10 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
         // contiguous runs, not message by message), then DMA'd; kernels start
         // as their pieces land and the planner's result is in
         for (uint64_t o = 0; o < bytes;) {
-          const uint64_t take = std::min(bytes - o, kChunkBytes);
+          const uint64_t take = std::min(bytes - o, slot_bytes);
           const unsigned si = slot_i++ & 1;
           HIPCHK(hipEventSynchronize(d.slot_free[si]));
+          if (slot_delay_us) std::this_thread::sleep_for(std::chrono::microseconds(slot_delay_us));
           const double g0 = now_ms();
           copy_threads(d.slot[si].as<uint8_t>(), arena + pos + o, take);
           const double g1 = now_ms();
@@ -2182,7 +2199,7 @@ void run_direct(msha_ctx* ctx, double t0, uint64_t n, const uint64_t* off, const
           if (!planned && event_done(d.ev_plan)) read_plan();
           if (planned) launch_upto(c);
         }
-      });
+      }, piece_bytes);
     for (; c < pieces; ++c) HIPCHK(hipEventRecord(d.span_ev[c], d.copy_stream));
     HIPCHK(hipEventRecord(d.ev_up1, d.copy_stream));
     d.st.h2d_payload_bytes = uploaded;
@@ -2726,10 +2743,19 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     bool clear_table = false;
     if (fold) {
       // epoch-tagged slots (plan.hip fold_claim): cleared only when the table
-      // is (re)allocated -- hipMalloc does not zero -- or the epoch wraps
-      const void* before = d.f_table.p;
+      // is (re)allocated -- hipMalloc does not zero -- or the epoch wraps. A
+      // reallocation is told by the capacity, not the pointer: hipFree then
+      // hipMalloc can hand back the same address, and the grown tail would then
+      // hold recycled words whose high half may equal the current epoch.
+      const uint64_t cap_before = d.f_table.cap;
       d.f_table.ensure(8 * cap);
-      if (d.f_table.p != before || d.f_epoch == 0xFFFFFFFFu) {
+      const bool grown = d.f_table.cap != cap_before;
+      // MSHA_POISON_FOLD_TABLE=1 (tests): a fresh allocation is filled with words
+      // tagged with the coming epoch, as recycled memory may be -- a table that
+      // was not cleared then claims garbage indices (tests/test_gpu_planned.py)
+      if (grown && env_u64("MSHA_POISON_FOLD_TABLE", 0))
+        HIPCHK(hipMemsetD32Async((hipDeviceptr_t)d.f_table.p, d.f_epoch + 1, d.f_table.cap / 4, st));
+      if (grown || d.f_epoch == 0xFFFFFFFFu) {
         clear_table = true;
         d.f_epoch = 0;
       }

@@ -165,7 +165,7 @@ __device__ __forceinline__ uint32_t lane_key(const PlanArgs& a, uint64_t i, uint
   const uint64_t end = a.dev_off[i] + (l ? l : 1) - 1;
   const uint64_t blocks = dev_blocks_for(l);
   const uint64_t region = a.long_blocks && blocks < a.long_blocks ? 1 : 0;
-  const uint32_t chunk = (uint32_t)(region * (a.chunks - a.pieces) + min((uint64_t)(end >> kDirectChunkShift),
+  const uint32_t chunk = (uint32_t)(region * (a.chunks - a.pieces) + min((uint64_t)(end >> a.piece_shift),
                                                                         a.pieces - 1));
   if (chunk_out) *chunk_out = chunk;
   return chunk * (uint32_t)a.B + (a.B > 1 ? (uint32_t)(a.bmax - blocks) : 0u);

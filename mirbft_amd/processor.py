@@ -294,7 +294,8 @@ def _epoch_change_aliases(reqs: Sequence[ActionHashRequest]) -> List[int]:
     message itself (recorder.go:39-47): the same object is the same payload.
     Acks off the wire hold equal copies: payloads from the same origin node
     with the same length are compared byte for byte (an altered copy is packed
-    and hashed on its own)."""
+    and hashed on its own), and so is a request whose object was seen before
+    but whose Data differs in length."""
     alias = [-1] * len(reqs)
     by_obj: dict = {}       # id(EpochChange) -> request index (objects live as long as reqs)
     by_content: dict = {}   # (origin node, length) -> [(index, payload)]
@@ -303,7 +304,10 @@ def _epoch_change_aliases(reqs: Sequence[ActionHashRequest]) -> List[int]:
         if not isinstance(t, HashOriginEpochChange):
             continue
         ec = t.epoch_change
-        if ec is not None and id(ec) in by_obj:
+        # the same object names the same payload only if the Data built from it
+        # has the same length (the contract is SHA-256(Data)); else compare bytes
+        if ec is not None and id(ec) in by_obj and \
+                sum(map(len, reqs[by_obj[id(ec)]].data)) == sum(map(len, r.data)):
             alias[i] = by_obj[id(ec)]
             continue
         data = b"".join(r.data)

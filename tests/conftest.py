@@ -14,6 +14,33 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (run with -m gpu on the GPU box)")
 
 
+def pytest_report_header(config):
+    """Name the library build the session runs (msha_build_id), so a failure log says
+    which build produced it."""
+    try:
+        from mirbft_amd import _lib
+        b = _lib.build_id()
+        return "libmirsha: %s (tree src %s, %s)" % (b["id"], b["tree_src"],
+                                                    "the tree's build" if b["matches_tree"] else "NOT the tree's build")
+    except Exception as ex:  # noqa: BLE001 -- a header must not fail the session
+        return "libmirsha: not loadable here (%s)" % ex
+
+
+def pytest_collection_modifyitems(config, items):
+    """A GPU session on a library that is not the tree's own build (an experiment's .so
+    left in place) is refused: its results would be reported as the product's.
+    MSHA_ALLOW_FOREIGN_LIB=1 runs it anyway (A/B runs of a variant build)."""
+    if not any(it.get_closest_marker("gpu") for it in items) or os.environ.get("MSHA_ALLOW_FOREIGN_LIB") == "1":
+        return
+    if getattr(config.option, "markexpr", "") != "gpu":
+        return
+    from mirbft_amd import _lib
+    b = _lib.build_id()
+    if not b["matches_tree"]:
+        raise pytest.UsageError("libmirsha.so is not this tree's build (%s; tree src %s): rebuild it "
+                                "(make -C mirbft_amd/csrc) or set MSHA_ALLOW_FOREIGN_LIB=1" % (b["id"], b["tree_src"]))
+
+
 def load_golden(name):
     with open(os.path.join(GOLDEN, name)) as f:
         return json.load(f)

@@ -29,7 +29,16 @@ def test_exports_via_nm():
 
 
 def test_abi_version():
-    assert L.lib().msha_abi_version() == L.ABI_VERSION == 8
+    assert L.lib().msha_abi_version() == L.ABI_VERSION == 9
+
+
+def test_build_id_is_the_trees():
+    """The built library says which sources it came from (msha_build_id), and they are
+    this tree's: a library left behind by an experiment (an A/B build copied over the
+    product .so, as round 4's wrong-digest log ran) is told apart from the product."""
+    b = L.build_id()
+    assert b["src"] and len(b["src"]) == 16 and "gfx950" in b["flags"], b
+    assert b["matches_tree"], b
 
 
 def test_library_is_gfx950_code_object():

@@ -134,3 +134,8 @@ def test_epoch_change_aliases_by_object_and_content():
             req(ec(1), 5), ActionHashRequest(data=epoch_change_hash_data(a), origin=HashOrigin(HashOriginBatch(0, 0, 1))),
             req(b, 1, 9)]
     assert _epoch_change_aliases(reqs) == [-1, 0, -1, 0, -1, 0, -1, -1, 2]
+    # the same object with Data built differently (another length): not an alias
+    # by identity -- the contract is SHA-256(Data) -- so its bytes are packed
+    short = ActionHashRequest(data=epoch_change_hash_data(a)[:-1],
+                              origin=HashOrigin(HashOriginEpochChange(source=7, origin=0, epoch_change=a)))
+    assert _epoch_change_aliases(reqs + [short]) == [-1, 0, -1, 0, -1, 0, -1, -1, 2, -1]

@@ -107,3 +107,27 @@ def test_long_chains_packed_last_run_as_heads(layout, shards, monkeypatch):
     # after the last piece, ~2 ms more)
     if shards == 1:
         assert max(tails) <= 1.0, (tails, tails_off)
+
+
+def test_lane_policy_runs_no_heads(layout):
+    """A context held to the lane kernel (MSHA_KERNEL_LANE) runs its long payloads as
+    ordinary lanes, as the device-planned path does: no head lanes, no cooperative or
+    two-lane launch, every digest exact."""
+    from mirbft_amd import Engine
+    arena, off, ln, exp = layout
+    eng = Engine(1)
+    try:
+        eng.set_kernel_policy("lane")
+        def pinned(a):
+            p = eng.pinned_empty(a.nbytes).view(a.dtype).reshape(a.shape)
+            p[...] = a
+            return p
+        out = eng.pinned_empty(32 * off.size).reshape(-1, 32)
+        st0 = eng.stats()
+        eng.digest_batch(pinned(arena), pinned(off), pinned(ln), out=out)
+        assert np.array_equal(out, exp)
+        st = eng.stats()
+        assert all(s["head_lanes"] == 0 for s in eng.shard_stats())
+        assert st["launches_coop"] == st0["launches_coop"]
+    finally:
+        eng.close()

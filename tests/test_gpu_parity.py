@@ -717,6 +717,39 @@ def test_staged_direct_pageable(shards, monkeypatch):
         assert e.stats()["staged_calls"] == st0["staged_calls"]
 
 
+@pytest.mark.parametrize("shards", [1, 3])
+def test_staged_direct_interleaved(shards, monkeypatch):
+    """The staged (pageable) direct path with its interleavings forced: 256 KiB
+    upload pieces, 128 KiB staging slots and a 40 us pause before each refill, so
+    the plan is read, the long payloads' heads start on the side stream and lane
+    groups launch between slot refills while later pieces still upload -- the
+    orderings a wrong digest there would come from (slot refill after its
+    slot_free event, a piece's event after all its bytes are queued, heads behind
+    their piece, the head D2H behind the last head; DESIGN.md (d) "The staged
+    path's orderings"). c5 batches with pageable and pinned off/len and digests:
+    every digest exact, the heads ran, and launches were issued before the last
+    staging copy (the interleaving happened)."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_VIRTUAL_SHARDS", str(shards))
+    monkeypatch.setenv("MSHA_DIRECT_PIECE_SHIFT", "18")
+    monkeypatch.setenv("MSHA_STAGED_SLOT_BYTES", str(128 << 10))
+    monkeypatch.setenv("MSHA_STAGED_DELAY_US", "40")
+    w = W.c5_storm(1 << 17)
+    exp = _oracle_dedup(w)
+    with Engine(1) as e:
+        for meta, outk in (("pageable", "pageable"), ("pinned", "pinned"), ("pageable", "pinned")):
+            off, ln = (w.off, w.len) if meta == "pageable" else (_pinned_copy(e, w.off), _pinned_copy(e, w.len))
+            out = None if outk == "pageable" else e.pinned_empty(w.n * 32).reshape(w.n, 32)
+            st0 = e.stats()
+            got = e.digest_batch(w.arena, off, ln, out=out)
+            assert np.array_equal(got, exp), _mismatch(w, got, exp, e, (meta, outk))
+            assert e.stats()["staged_calls"] == st0["staged_calls"] + 1
+            sh = e.shard_stats()
+            assert all(s["head_lanes"] > 0 for s in sh), sh
+            # a kernel was queued before the shard's last staging copy ended
+            assert all(0 < s["first_launch_ms"] < s["gather_end_ms"] for s in sh), sh
+
+
 def _pinned_batch(e, lens, offs=None, seed=21):
     """A pinned arena holding messages of the given lengths (16-byte aligned starts
     unless offs is given) and the oracle's digests."""

@@ -142,6 +142,22 @@ def test_one_payload_aliased(engine, n):
     assert np.array_equal(_run(engine, w, False), exp)
 
 
+def test_fold_table_grows_after_small_calls(monkeypatch):
+    """The epoch-tagged alias table (plan.hip fold_claim) must be cleared whenever it
+    grows, whatever address the new allocation gets (a regrown
+    table at the old address kept its uncleared tail). Small folded calls move the
+    epoch past 1, then a larger call grows the table; MSHA_POISON_FOLD_TABLE fills
+    the fresh allocation with words tagged with the coming epoch, as recycled
+    memory may hold, so a table left uncleared claims garbage indices. Every digest
+    of every call must be exact."""
+    from mirbft_amd import Engine
+    monkeypatch.setenv("MSHA_POISON_FOLD_TABLE", "1")
+    with Engine(1) as e:
+        for n in (4096, 4096, 4096, 1 << 18, 1 << 18, 1 << 19):
+            w = W.c5_storm(n)
+            assert np.array_equal(_run(e, w, True), _expect(w)), n
+
+
 def test_empty_and_boundary_lengths(engine):
     lens = np.array([0, 0, 1, 55, 56, 63, 64, 65, 119, 120, 0, 128, 4096 * 64 - 9, 4096 * 64,
                      300_000, 1 << 20, 0] * 50, dtype=np.uint64)

@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
           const uint64_t a = bounds[s], m = bounds[s + 1] - a;
           std::vector<uint8_t> mark(nG, 0);
           const ShardSpan sh = stage_and_mark(off.data() + a, len.data() + a, m, glo, gs, nullptr, nullptr, mark,
-                                              long_chain_blocks(sc.bmax));
+                                              long_chain_blocks(sc.bmax, MSHA_KERNEL_AUTO));
           std::vector<uint64_t> gmap(sh.g1 - sh.g0 + 1);
           build_gmap(mark, sh.g0, gmap.size(), gs, gmap.data());
           done[s] = now_ms() - t1;
