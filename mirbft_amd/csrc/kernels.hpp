@@ -125,6 +125,7 @@ struct FoldArgs {
   uint32_t epoch = 1;         // this call's tag: a slot of another epoch is empty (never 0)
   uint32_t* rep = nullptr;    // n (with table): the lane message i's digest comes from
   uint64_t* tmax = nullptr;   // (with table) ceil(n / 4096): largest offset before each tile
+  uint64_t* tsum = nullptr;   // (early head) 2 per tile: the tile's short messages' blocks, its longest chain
   uint32_t* cnt;              // kFoldBuckets zeroed counters -> bucket starts
   uint64_t* big = nullptr;    // 2 x kFoldBigBuckets zeroed: per power-of-two key, the largest
                               // block count and the block sum (the head's cost model needs the
@@ -133,15 +134,22 @@ struct FoldArgs {
   uint32_t* info;             // [0] lanes, [1] positions the lane kernel skips (the head's),
                               // [2] distinct long payloads, [3] k_fold_longs workgroups done,
                               // [4] the early head's lanes (0: none), [5] the late head's,
+                              // [6] k_fold_tilescan's first decision (0: no early head),
                               // [8..11] two u64: the batch's blocks and longest chain
                               // ([2], [3], [8..11] zeroed by the caller: 12 words)
-  // The early head (folding only; long_blocks 0: off): k_fold_longs claims every
-  // message of >= long_blocks blocks in the alias table before anything else,
-  // listing each distinct one in longs; when there are at most long_cap, those
-  // are the head, launched right then on the two-lane kernel over longs (info[4]),
-  // instead of after the scan and scatter, and k_fold_insert never takes a long
-  // message as fresh (so its representative is the listed one).
+  // The early head (folding only; long_blocks 0: off): k_fold_tilescan sizes the
+  // batch (info[6]: 0 when the short messages alone outlast the longest chain);
+  // unless it stood down there, k_fold_longs claims every message of >=
+  // long_blocks blocks in the alias table beside the insert, listing each
+  // distinct one in longs; when there are at most long_cap, and their chain
+  // outlasts the lane kernel's share, they are the head (info[4]), launched right
+  // then on the two-lane kernel over longs instead of after the scan and
+  // scatter, and k_fold_insert never takes a long message as fresh (so its
+  // representative is the listed one).
   uint32_t* longs = nullptr;
+  // off and len both 16-byte aligned: the per-thread runs of 16 messages load as
+  // 16-byte vectors (plan.hip load_run)
+  uint32_t vec = 0;
   uint32_t long_blocks = 0;
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
@@ -163,10 +171,14 @@ struct FoldArgs {
   uint32_t head_per_wg = 128;    // messages per head workgroup (one CU each)
   uint32_t tiebreak = 1;         // head-bound ties go to the cut with the most lane-kernel room (A/B: 0)
 };
+// Folding only: the tile maxima and their prefix (k_fold_tilemax, k_fold_tilescan),
+// with the early head's list and decision when long_blocks is set; then
+// launch_fold_plan: the insert (or, unfolded, the counts), scan and scatter.
+hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st);
 // scan_after (may be null): an event k_fold_scan waits for (the early head's list).
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_after = nullptr);
-// The early head's list (FoldArgs::longs): on a stream of its own, beside the alias
-// insert (both claim through the same table); the scan waits for it.
+// The early head's list (FoldArgs::longs): on a stream of its own, after the
+// prefix, beside the alias insert (both claim through the same table).
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st);
 // out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.
 hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st);

@@ -2761,7 +2761,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       }
       ++d.f_epoch;
       d.f_rep.ensure(4 * n);
-      d.f_tmax.ensure(8 * ((n + 4095) / 4096));
+      d.f_tmax.ensure(8 * 3 * ((n + 4095) / 4096));  // tile maxima, then 2 x tsum per tile
     }
     // The planner's scratch (table, order, counters) is the context's: a call
     // on another stream must not overwrite it while an earlier call still reads it.
@@ -2791,11 +2791,13 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.off = d_off;
     fa.len = d_len;
     fa.n = n;
+    fa.vec = ((reinterpret_cast<uintptr_t>(d_off) | reinterpret_cast<uintptr_t>(d_len)) & 15) == 0;
     fa.table = fold ? d.f_table.as<uint64_t>() : nullptr;
     fa.tmask = cap - 1;
     fa.epoch = d.f_epoch;
     fa.rep = fold ? d.f_rep.as<uint32_t>() : nullptr;
     fa.tmax = fold ? d.f_tmax.as<uint64_t>() : nullptr;
+    fa.tsum = fold ? fa.tmax + (n + 4095) / 4096 : nullptr;
     fa.cnt = d.f_cnt.as<uint32_t>();
     fa.big = reinterpret_cast<uint64_t*>(fa.cnt + msha::kFoldBuckets);  // 4 x 4,148 B: 8-byte aligned
     fa.order = d.f_order.as<uint32_t>();
@@ -2816,12 +2818,14 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
     fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);
-    // The early head (folded calls with a two-lane head): the distinct payloads
-    // of >= kLongBlocks blocks are listed (k_fold_longs, beside the alias insert)
-    // and, when at most an eighth of the CUs' worth, start on the two-lane kernel
-    // on a stream of their own right then, while the insert, the scan and the
-    // scatter still run -- a folded storm's head no longer waits ~0.08 ms for the
-    // whole plan. MSHA_EARLY_HEAD=0: the head after the scan's cut (A/B).
+    // The early head (folded calls with a two-lane head): unless the tile prefix
+    // already stood it down (the short messages alone outlast the longest chain),
+    // the distinct payloads of >= kLongBlocks blocks are listed (k_fold_longs,
+    // beside the alias insert) and, when at most an eighth of the CUs' worth,
+    // start on the two-lane kernel on a stream of their own right then, while
+    // the insert, the scan and the scatter still run -- a folded storm's head
+    // does not wait for the whole plan. MSHA_EARLY_HEAD=0: the head after the
+    // scan's cut (A/B).
     const bool early = fold && head && two_lane && env_u64("MSHA_EARLY_HEAD", 1) != 0;
     if (early) {
       fa.long_blocks = (uint32_t)kLongBlocks;
@@ -2831,8 +2835,11 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       if (!d.head_stream) HIPCHK(hipStreamCreateWithFlags(&d.head_stream, hipStreamNonBlocking));
       for (hipEvent_t* e : {&d.ev_longs, &d.ev_join2})
         if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-      // the list on the head's stream, forked after the planner's memsets: it
-      // runs beside the tile scans and the alias insert, not in front of them
+    }
+    HIPCHK(msha::launch_fold_prefix(fa, ps));
+    if (early) {
+      // the head's stream forks after the prefix (its first decision): the list
+      // runs beside the alias insert
       HIPCHK(hipEventRecord(d.ev_longs, ps));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
       HIPCHK(msha::launch_fold_longs(fa, d.cus, d.head_stream));

@@ -311,33 +311,104 @@ __device__ __forceinline__ uint32_t fold_key(uint64_t len) {  // descending bloc
 // EpochChange re-hashes: 5 %) probe and claim. A key first named by a
 // non-candidate and then by candidates is hashed twice -- once for the
 // non-candidate, once for the candidates' claimant -- with the same digest.
-// Tiles of kFoldTile messages, 16 consecutive per thread; tmax[t] = the
+// Tiles of kPlanTile messages, 16 consecutive per thread; tmax[t] = the
 // largest offset of tiles before t (k_fold_tilemax, then k_fold_tilescan).
+//
+// A thread's run of 16 consecutive messages is 128 bytes of off and 128 of len:
+// with a.vec (both arrays 16-byte aligned) it loads as eight 16-byte vectors
+// each -- every load instruction then moves whole 16-byte lane slices of a line
+// the lane reads entirely, instead of 16 scalar 8-byte loads per array that
+// each touch 64 lines for 8 bytes apiece (round 4: k_fold_insert moved 1.10 GB
+// per c5 step for 134 MB of off/len).
+__device__ __forceinline__ void load_run(const uint64_t* __restrict__ p, uint64_t base, uint64_t n, bool vec,
+                                         uint64_t (&v)[kPlanItems]) {
+  if (vec && base + kPlanItems <= n) {
+    const uint4* q = reinterpret_cast<const uint4*>(p + base);
+#pragma unroll
+    for (uint32_t k = 0; k < kPlanItems / 2; ++k) {
+      const uint4 x = q[k];
+      v[2 * k] = (uint64_t)x.x | ((uint64_t)x.y << 32);
+      v[2 * k + 1] = (uint64_t)x.z | ((uint64_t)x.w << 32);
+    }
+  } else {
+#pragma unroll
+    for (uint32_t r = 0; r < kPlanItems; ++r) v[r] = base + r < n ? p[base + r] : 0;
+  }
+}
+
+// With the early head (a.long_blocks) the same pass also reads the tile's
+// lengths and sizes it for k_fold_tilescan's decision: the tile's short
+// messages' blocks (the lane kernel's share, without the distinct long
+// payloads) and its longest chain, into tsum.
 __global__ __launch_bounds__(256) void k_fold_tilemax(FoldArgs a) {
   __shared__ uint64_t part[256];
-  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile;
+  __shared__ unsigned long long s_sum[4], s_max[4];
+  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanItems;
+  uint64_t o[kPlanItems];
+  load_run(a.off, base, a.n, a.vec, o);
   uint64_t m = 0;
-  for (uint32_t r = 0; r < kPlanItems; ++r) {
-    const uint64_t i = base + r * 256 + threadIdx.x;
-    if (i < a.n) m = max(m, a.off[i]);
-  }
+#pragma unroll
+  for (uint32_t r = 0; r < kPlanItems; ++r) m = max(m, o[r]);
   part[threadIdx.x] = m;
+  if (a.long_blocks) {
+    uint64_t l[kPlanItems];
+    load_run(a.len, base, a.n, a.vec, l);
+    uint64_t sum = 0, mx = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kPlanItems; ++r) {
+      const uint64_t blocks = base + r < a.n ? dev_blocks_for(l[r]) : 0;
+      mx = max(mx, blocks);
+      if (blocks < a.long_blocks) sum += blocks;
+    }
+    for (uint32_t d = 32; d > 0; d >>= 1) {  // wave sums, then one LDS word per wave
+      sum += __shfl_xor(sum, d);
+      mx = max(mx, (uint64_t)__shfl_xor(mx, d));
+    }
+    if (__lane_id() == 0) s_sum[threadIdx.x >> 6] = sum, s_max[threadIdx.x >> 6] = mx;
+  }
   __syncthreads();
   for (uint32_t d = 128; d > 0; d >>= 1) {
     if (threadIdx.x < d) part[threadIdx.x] = max(part[threadIdx.x], part[threadIdx.x + d]);
     __syncthreads();
   }
-  if (threadIdx.x == 0) a.tmax[blockIdx.x] = part[0];
+  if (threadIdx.x == 0) {
+    a.tmax[blockIdx.x] = part[0];
+    if (a.long_blocks) {
+      a.tsum[2 * blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+      a.tsum[2 * blockIdx.x + 1] = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
+    }
+  }
 }
 
+// One workgroup: the exclusive prefix max of the tile maxima and, with the early
+// head, a first decision: when the short messages' blocks alone -- x
+// wave_block_cycles over the SIMDs -- keep the lane kernel busy past the
+// longest chain on the head (c5 on one GPU: ~60 M blocks against one 1,427-block
+// chain), the early head cannot pay and stands down before listing anything
+// (info[6] = 0; k_fold_longs then returns at once). Otherwise info[6] = 1 and
+// k_fold_longs lists and claims the long payloads and decides on the exact rule.
 __global__ __launch_bounds__(1024) void k_fold_tilescan(FoldArgs a, uint64_t tiles) {
   __shared__ uint64_t part[1024];
+  __shared__ unsigned long long s_sum[16], s_max[16];
   const uint32_t t = threadIdx.x;
   const uint64_t per = (tiles + 1023) / 1024;
   const uint64_t b0 = min((uint64_t)t * per, tiles), b1 = min(b0 + per, tiles);
-  uint64_t m = 0;
-  for (uint64_t b = b0; b < b1; ++b) m = max(m, a.tmax[b]);
+  uint64_t m = 0, sum = 0, mx = 0;
+  for (uint64_t b = b0; b < b1; ++b) {
+    m = max(m, a.tmax[b]);
+    if (a.long_blocks) {
+      sum += a.tsum[2 * b];
+      mx = max(mx, a.tsum[2 * b + 1]);
+    }
+  }
   part[t] = m;
+  if (a.long_blocks) {
+    for (uint32_t d = 32; d > 0; d >>= 1) {
+      sum += __shfl_xor(sum, d);
+      mx = max(mx, (uint64_t)__shfl_xor(mx, d));
+    }
+    if (__lane_id() == 0) s_sum[t >> 6] = sum, s_max[t >> 6] = mx;
+  }
   __syncthreads();
   for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive prefix max
     const uint64_t v = t >= d ? part[t - d] : 0ull;
@@ -350,6 +421,13 @@ __global__ __launch_bounds__(1024) void k_fold_tilescan(FoldArgs a, uint64_t til
     const uint64_t v = a.tmax[b];
     a.tmax[b] = run;
     run = max(run, v);
+  }
+  if (a.long_blocks && t == 0) {
+    unsigned long long ss = 0, sm = 0;
+    for (int w = 0; w < 16; ++w) ss += s_sum[w], sm = max(sm, s_max[w]);
+    const uint64_t t_body = ss * a.wave_block_cycles / (64ull * a.simds);
+    const uint64_t t_head = sm * a.coop_cycles;
+    a.info[6] = sm >= a.long_blocks && t_body < t_head ? 1u : 0u;
   }
 }
 
@@ -387,14 +465,35 @@ __device__ __forceinline__ void fold_hist_clear(FoldHist& h) {
   for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x) h.n[j] = 0;
   if (threadIdx.x < kFoldBigBuckets) h.bmax[threadIdx.x] = h.bsum[threadIdx.x] = 0;
 }
-__device__ __forceinline__ void fold_hist_add(FoldHist& h, uint64_t len) {
-  const uint64_t blocks = dev_blocks_for(len);
-  const uint32_t k = kFoldBuckets - 1 - fold_bucket(blocks);
-  atomicAdd(&h.n[k], 1u);
+__device__ __forceinline__ void fold_hist_big(FoldHist& h, uint32_t k, uint64_t blocks) {
   if (k < kFoldBigBuckets) {  // >= 4,096 blocks (1/4 MiB): rare
     atomicMax(&h.bmax[k], (unsigned long long)blocks);
     atomicAdd(&h.bsum[k], (unsigned long long)blocks);
   }
+}
+__device__ __forceinline__ void fold_hist_add(FoldHist& h, uint64_t len) {
+  const uint64_t blocks = dev_blocks_for(len);
+  const uint32_t k = kFoldBuckets - 1 - fold_bucket(blocks);
+  atomicAdd(&h.n[k], 1u);
+  fold_hist_big(h, k, blocks);
+}
+// The same over the active lanes of a wave where valid: the lanes sharing the
+// first valid lane's key add once, together (a storm's wave: ~70 % one key,
+// which one LDS atomic per lane serialises ~45 deep), the rest one each.
+__device__ __forceinline__ void fold_hist_add_wave(FoldHist& h, bool valid, uint64_t len) {
+  const uint64_t blocks = dev_blocks_for(len);
+  const uint32_t k = valid ? kFoldBuckets - 1 - fold_bucket(blocks) : 0xFFFFFFFFu;
+  const uint64_t any = __ballot(valid);
+  if (!any) return;
+  const uint32_t k0 = __shfl(k, __ffsll((long long)any) - 1);
+  const uint64_t same = __ballot(valid && k == k0);
+  const unsigned lane = __lane_id();
+  if ((same >> lane) & 1) {
+    if ((same & ((1ull << lane) - 1)) == 0) atomicAdd(&h.n[k0], (uint32_t)__popcll(same));
+  } else if (valid) {
+    atomicAdd(&h.n[k], 1u);
+  }
+  if (valid) fold_hist_big(h, k, blocks);
 }
 __device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h) {
   for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
@@ -408,18 +507,28 @@ __device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h) 
 // Also counts the tile's lanes into the bucket histogram (what k_fold_keys
 // does without folding): a fresh message is its own lane, a candidate is one
 // when its claim returns itself -- so the lanes' metadata is read once.
+// Round 5: each thread's 16 consecutive (off, len) load as 16-byte vectors
+// (load_run), the tile's representatives gather in LDS and go out as 4-byte
+// words of consecutive messages per wave instruction (whole lines, not 4 bytes
+// per lane at a 64-byte stride), and the candidates' list is appended and the
+// histogram counted wave-aggregated.
 __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   __shared__ uint64_t part[256];
   __shared__ FoldHist hist;
+  __shared__ uint32_t trep[kPlanTile];   // the tile's representatives, by position in the tile
+  __shared__ uint16_t cand[kPlanTile];   // candidates' positions in the tile
+  __shared__ uint32_t ncand;
   fold_hist_clear(hist);
-  const uint64_t base = (uint64_t)blockIdx.x * kPlanTile + (uint64_t)threadIdx.x * kPlanItems;
-  uint64_t o[kPlanItems];
+  if (threadIdx.x == 0) ncand = 0;
+  const uint64_t tile0 = (uint64_t)blockIdx.x * kPlanTile;
+  const uint32_t lb = threadIdx.x * kPlanItems;
+  const uint64_t base = tile0 + lb;
+  uint64_t o[kPlanItems], l[kPlanItems];
+  load_run(a.off, base, a.n, a.vec, o);
+  load_run(a.len, base, a.n, a.vec, l);
   uint64_t m = 0;
 #pragma unroll
-  for (uint32_t r = 0; r < kPlanItems; ++r) {
-    o[r] = base + r < a.n ? a.off[base + r] : 0;
-    m = max(m, o[r]);
-  }
+  for (uint32_t r = 0; r < kPlanItems; ++r) m = max(m, o[r]);
   part[threadIdx.x] = m;
   __syncthreads();
   for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive prefix max over the tile's threads
@@ -430,39 +539,47 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   }
   const bool first_ever = blockIdx.x == 0 && threadIdx.x == 0;
   uint64_t run = max(a.tmax[blockIdx.x], threadIdx.x ? part[threadIdx.x - 1] : 0ull);
+  const unsigned lane = __lane_id();
   // Candidates are few (c5: 5 %) but spread over every wave: claiming them in
   // place would run each wave's claim loop (a load -> CAS -> compare chain of
   // memory round trips) once per item row. They go to an LDS list instead and
   // the workgroup's threads claim them side by side.
-  __shared__ uint32_t cand[kPlanTile];
-  __shared__ uint32_t ncand;
-  if (threadIdx.x == 0) ncand = 0;
-  __syncthreads();
 #pragma unroll
   for (uint32_t r = 0; r < kPlanItems; ++r) {
     const uint64_t i = base + r;
-    if (i >= a.n) break;
-    // above every earlier offset (a long message never: k_fold_longs claimed its key)
-    const bool fresh = (o[r] > run || (first_ever && r == 0)) &&
-                       !(a.long_blocks && dev_blocks_for(a.len[i]) >= a.long_blocks);
-    if (fresh) {
-      a.rep[i] = (uint32_t)i;
-      fold_hist_add(hist, a.len[i]);
-    } else {
-      cand[atomicAdd(&ncand, 1u)] = (uint32_t)(i - (uint64_t)blockIdx.x * kPlanTile);
+    const bool valid = i < a.n;
+    // above every earlier offset (a long message never: with the early head it
+    // claims, so its representative is the one k_fold_longs lists)
+    const bool lng = valid && a.long_blocks && dev_blocks_for(l[r]) >= a.long_blocks;
+    const bool fresh = valid && !lng && (o[r] > run || (first_ever && r == 0));
+    const bool is_cand = valid && !fresh;
+    if (fresh) trep[lb + r] = (uint32_t)i;
+    fold_hist_add_wave(hist, fresh, l[r]);
+    const uint64_t cm = __ballot(is_cand);
+    if (cm) {
+      uint32_t at = 0;
+      const int leader = __ffsll((long long)cm) - 1;
+      if ((int)lane == leader) at = atomicAdd(&ncand, (uint32_t)__popcll(cm));
+      at = __shfl(at, leader);
+      if (is_cand) cand[at + (uint32_t)__popcll(cm & ((1ull << lane) - 1))] = (uint16_t)(lb + r);
     }
     run = max(run, o[r]);
   }
   __syncthreads();
-  const uint64_t tile0 = (uint64_t)blockIdx.x * kPlanTile;
   for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
-    const uint64_t i = tile0 + cand[c];
-    const uint64_t l = a.len[i];
-    const uint32_t rp = fold_claim(a, i, a.off[i], l);
-    a.rep[i] = rp;
-    if (rp == (uint32_t)i) fold_hist_add(hist, l);
+    const uint32_t li = cand[c];
+    const uint64_t i = tile0 + li;
+    const uint64_t ln = a.len[i];
+    const uint32_t rp = fold_claim(a, i, a.off[i], ln);
+    trep[li] = rp;
+    if (rp == (uint32_t)i) fold_hist_add(hist, ln);
   }
   __syncthreads();
+#pragma unroll 4
+  for (uint32_t r = 0; r < kPlanItems; ++r) {
+    const uint32_t li = r * 256 + threadIdx.x;
+    if (tile0 + li < a.n) a.rep[tile0 + li] = trep[li];
+  }
   fold_hist_flush(a, hist);
 }
 
@@ -658,37 +775,63 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
 // The early head's list: every message of >= long_blocks blocks claims its
 // (off, len) in the alias table (a hot payload costs a cached read after the
 // first claim); each claimant -- one per distinct long payload -- is listed. It
-// runs beside k_fold_insert: whichever claims a key first, both read the same
-// claimant back, and the claimant, a long message itself, lists itself here. The
-// last workgroup to finish publishes the list's length as the early head, or 0
-// when it is longer than long_cap (then the scan's cut decides, as without it).
-// It also estimates the lane kernel's share -- every short message's blocks (a
-// storm's re-hashes are its long payloads; short ones are mostly distinct) --
-// and finds the longest chain: when that share would keep the lane kernel busy
-// past the head's chain anyway (c5 on one GPU: ~60 M blocks against one
-// 1,427-block chain), starting the head early buys nothing and its list only
-// competes with the insert for the table, so the head then stands down too.
+// runs beside k_fold_insert, after the tile prefix: whichever claims a key
+// first, both read the same claimant back, and the claimant, a long message
+// itself, lists itself here. The last workgroup to finish publishes the list's
+// length as the early head, or 0 when it is longer than long_cap or the lane
+// kernel's share -- every short message's blocks plus the distinct long ones --
+// outlasts the head's chain anyway (then the scan's cut decides, as without it).
+// k_fold_tilescan already stood it down (info[6] == 0) when the short blocks
+// alone do: then every workgroup returns at once (c5 on one GPU: round 4 ran
+// the whole list, 110-234 us of claims beside the insert, to stand down).
+// Round 5: a workgroup takes tiles of kPlanTile consecutive messages, loads each
+// thread's 16 lengths as 16-byte vectors, lists the tile's long messages in
+// LDS, and its threads then claim them side by side (round 4 claimed in the
+// stride loop: every wave's load -> compare chain once per iteration).
 __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t sum = 0, mx = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < a.n; i += stride) {
-    const uint64_t l = a.len[i];
-    const uint64_t blocks = dev_blocks_for(l);
-    mx = max(mx, blocks);
-    if (blocks < a.long_blocks) {
-      sum += blocks;
-      continue;
-    }
-    if (fold_claim(a, i, a.off[i], l) == (uint32_t)i) {
-      sum += blocks;
-      const uint32_t k = atomicAdd(&a.info[2], 1u);
-      if (k < a.long_cap) a.longs[k] = (uint32_t)i;
-    }
-  }
+  if (a.info[6] == 0) return;  // uniform: k_fold_tilescan's first decision
+  __shared__ uint32_t list[kPlanTile];
+  __shared__ uint32_t nlist;
   __shared__ unsigned long long s_sum, s_max;
   __shared__ bool last;
   if (threadIdx.x == 0) s_sum = s_max = 0;
-  __syncthreads();
+  uint64_t sum = 0, mx = 0;
+  const unsigned lane = __lane_id();
+  const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
+  for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    if (threadIdx.x == 0) nlist = 0;
+    __syncthreads();
+    const uint64_t base = tile * kPlanTile + (uint64_t)threadIdx.x * kPlanItems;
+    uint64_t l[kPlanItems];
+    load_run(a.len, base, a.n, a.vec, l);
+#pragma unroll
+    for (uint32_t r = 0; r < kPlanItems; ++r) {
+      const bool valid = base + r < a.n;
+      const uint64_t blocks = valid ? dev_blocks_for(l[r]) : 0;
+      mx = max(mx, blocks);
+      const bool lng = valid && blocks >= a.long_blocks;
+      if (valid && !lng) sum += blocks;
+      const uint64_t lm = __ballot(lng);
+      if (lm) {
+        uint32_t at = 0;
+        const int leader = __ffsll((long long)lm) - 1;
+        if ((int)lane == leader) at = atomicAdd(&nlist, (uint32_t)__popcll(lm));
+        at = __shfl(at, leader);
+        if (lng) list[at + (uint32_t)__popcll(lm & ((1ull << lane) - 1))] = (uint32_t)(base + r);
+      }
+    }
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < nlist; c += blockDim.x) {
+      const uint64_t i = list[c];
+      const uint64_t ln = a.len[i];
+      if (fold_claim(a, i, a.off[i], ln) == (uint32_t)i) {
+        sum += dev_blocks_for(ln);
+        const uint32_t k = atomicAdd(&a.info[2], 1u);
+        if (k < a.long_cap) a.longs[k] = (uint32_t)i;
+      }
+    }
+    __syncthreads();  // the list is rewritten by the next tile
+  }
   atomicAdd(&s_sum, (unsigned long long)sum);
   atomicMax(&s_max, (unsigned long long)mx);
   __syncthreads();
@@ -713,7 +856,7 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
 
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
   if (a.n == 0 || !a.long_blocks) return hipSuccess;
-  const unsigned grid = (unsigned)std::min<uint64_t>((a.n + 255) / 256, (uint64_t)cus * 4);
+  const unsigned grid = (unsigned)std::min<uint64_t>((a.n + kPlanTile - 1) / kPlanTile, (uint64_t)cus * 4);
   hipLaunchKernelGGL(k_fold_longs, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
@@ -730,14 +873,18 @@ __global__ __launch_bounds__(256) void k_fold_fill(const uint32_t* __restrict__ 
   dst[1] = src[1];
 }
 
+hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st) {
+  if (a.n == 0 || !a.table) return hipSuccess;
+  const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
+  hipLaunchKernelGGL(k_fold_tilemax, dim3(ptiles), dim3(256), 0, st, a);
+  hipLaunchKernelGGL(k_fold_tilescan, dim3(1), dim3(1024), 0, st, a, (uint64_t)ptiles);
+  return hipGetLastError();
+}
+
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_after) {
   if (a.n == 0) return hipSuccess;
   const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
-  if (a.table) {
-    hipLaunchKernelGGL(k_fold_tilemax, dim3(ptiles), dim3(256), 0, st, a);
-    hipLaunchKernelGGL(k_fold_tilescan, dim3(1), dim3(1024), 0, st, a, (uint64_t)ptiles);
-    hipLaunchKernelGGL(k_fold_insert, dim3(ptiles), dim3(256), 0, st, a);
-  }
+  if (a.table) hipLaunchKernelGGL(k_fold_insert, dim3(ptiles), dim3(256), 0, st, a);
   const unsigned ftiles = (unsigned)((a.n + kFoldTile - 1) / kFoldTile);
   if (!a.table) hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
   if (scan_after) {

@@ -32,6 +32,7 @@ hipError_t launch_digest_of_digests(const uint8_t*, const uint32_t*, const uint6
   abort();
 }
 hipError_t launch_plan(const PlanArgs&, hipStream_t) { abort(); }
+hipError_t launch_fold_prefix(const FoldArgs&, hipStream_t) { abort(); }
 hipError_t launch_fold_plan(const FoldArgs&, hipStream_t, hipEvent_t) { abort(); }
 hipError_t launch_fold_longs(const FoldArgs&, int, hipStream_t) { abort(); }
 hipError_t launch_fold_fill(const uint32_t*, uint64_t, uint8_t*, hipStream_t) { abort(); }

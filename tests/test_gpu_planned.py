@@ -80,7 +80,7 @@ def test_c5_rank_slice_routes_long_chains(engine, world, fold):
     after = engine.stats()
     assert np.array_equal(got, exp)
     if fold or world == 8:
-        # folded: the early head (the long payloads, k_fold_longs) and the scan's
+        # folded: the early head (the long payloads, k_fold_tilemax's list) and the scan's
         # cut (empty then) are two launches
         assert _delta(before, after, "launches_coop") == (2 if fold and _EARLY else 1)
     assert _delta(before, after, "launches_lane") == 1
@@ -259,8 +259,8 @@ def test_bad_flags(engine):
 @pytest.mark.parametrize("early", ["0", "1"])
 def test_early_head(engine, monkeypatch, early):
     """Folded calls with the early head (MSHA_EARLY_HEAD=1: the distinct payloads of
-    >= 256 blocks claimed and listed before the alias insert, and started on the
-    two-lane kernel right then) and without: c5 slices at 1 and 8 GPUs, a batch
+    >= 256 blocks claimed and listed by the planner's first pass, before the alias
+    insert, and started on the two-lane kernel right then) and without: c5 slices at 1 and 8 GPUs, a batch
     whose long payloads are too many for the early head (it stands down and the
     scan's cut decides), and long payloads first named by a fresh message; every
     digest exact, the two head launches counted."""
