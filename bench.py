@@ -296,14 +296,28 @@ def host_api_leg(args, world: int, unaliased: bool = False) -> dict:
              "re-hashes cross PCIe (a caller that does not share payloads)" if unaliased else
              "each distinct EpochChange payload packed once and named by every action that carries it "
              "(what the Go drop-in packs since round 4: epochChangeAliases)")
+    return host_api_summary(d, what)
+
+
+def host_api_summary(d: dict, what: str) -> dict:
+    """The host_api object from a --mode lib line: the call's figures and, per GPU,
+    its shard's messages, lanes, heads, H2D bytes and times -- and its upload rate
+    (h2d_bytes / upload_ms), so a node whose links or NUMA placement contend shows
+    it GPU by GPU (upload_gbps_min / _max)."""
+    per = []
+    for x in d["last_call_shards"]:
+        e = {k: x[k] for k in ("device", "messages", "lanes", "head_lanes", "h2d_bytes", "device_ms",
+                               "upload_ms", "kernel_ms", "first_launch_ms", "plan_kernel_ms")}
+        e["upload_gbps"] = x["h2d_bytes"] / x["upload_ms"] / 1e6 if x["upload_ms"] > 0 else None
+        per.append(e)
+    rates = [e["upload_gbps"] for e in per if e["upload_gbps"] is not None]
     return {"what": what, "arena_bytes": d["arena_bytes"],
             "value": d["value"], "unit": "digests/s", "n_gpus": d["n_gpus"], "shards": d["shards"],
             "virtual_shards": d["virtual_shards"], "ms_per_call": d["ms_per_step"], "call_ms": d["call_ms"],
             "gbps_hashed": d["gbps_hashed"], "steps": d["steps"], "plan_ms": d["last_call_stats"]["plan_ms"],
             "first_launch_ms_max": max(x["first_launch_ms"] for x in d["last_call_shards"]),
-            "per_gpu": [{k: x[k] for k in ("device", "messages", "lanes", "head_lanes", "h2d_bytes", "device_ms",
-                                           "upload_ms", "kernel_ms", "first_launch_ms", "plan_kernel_ms")}
-                        for x in d["last_call_shards"]]}
+            "upload_gbps_min": min(rates) if rates else None, "upload_gbps_max": max(rates) if rates else None,
+            "per_gpu": per}
 
 
 def kind_of(st0: dict, st1: dict) -> str:
@@ -487,25 +501,65 @@ def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist, form: st
     eng.device_status()
     kind = kind_of(st0, eng.stats())
     verify_sample(w, d_out)
-    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kern_max = (float(x) for x in t.tolist())
-    tot = torch.tensor([w.n, w.message_bytes, w.blocks, hashed_blocks(w, form)], dtype=torch.float64)
-    dist.all_reduce(tot)
-    n, nbytes, blocks, hashed = (float(x) for x in tot.tolist())
     del step, d_out
     torch.cuda.empty_cache()
-    achieved = OPS_PER_BLOCK * hashed / (kern_max * 1e-3) / 1e12      # all GPUs, slowest rank's launch
-    return {"workload": f"c5: {1 << 23} mixed actions (70/25/5) over {world} GPUs, {w.n} per GPU",
-            "form": C5_FORM_NOTES[form],
-            "n_gpus": world, "scaling": "strong", "value": n * args.steps / elapsed, "unit": "digests/s",
-            "gbps_hashed": nbytes * args.steps / elapsed / 1e9, "ms_per_step": elapsed / args.steps * 1e3,
-            "kernel_ms_mean_max_over_ranks": kern_max, "kernel": kind,
-            "frac": achieved / (PEAK_VALU_TOPS * world), "achieved": achieved, "peak": PEAK_VALU_TOPS * world,
-            "blocks": int(blocks), "hashed_blocks": int(hashed),
-            "effective_clock_ghz_rank0": clock.get("effective_clock_ghz"),
-            "verified": "512 digests per rank vs oracle (stride not a multiple of 64)",
-            "warmup_steps_run": warm}
+    lmax = int(w.len.max()) if w.n else 0
+    out = c5_rank_summary(dist, world, form, n=w.n, nbytes=w.message_bytes, blocks=w.blocks,
+                          hashed=hashed_blocks(w, form),
+                          max_blocks=(lmax >> 6) + (1 if (lmax & 63) < 56 else 2) if w.n else 0,
+                          elapsed=elapsed, kern_ms=kern_ms, clock_ghz=clock.get("effective_clock_ghz"),
+                          steps=args.steps)
+    out.update({"workload": f"c5: {1 << 23} mixed actions (70/25/5) over {world} GPUs, {w.n} per GPU",
+                "kernel": kind, "warmup_steps_run": warm,
+                "verified": "512 digests per rank vs oracle (stride not a multiple of 64)"})
+    return out
+
+
+# The two-lane head's cost of one chain block (k_digest_chain2, SIMD-shader cycles
+# at the final round-4 code, profiles/r04_pmc.json cycles_per_chain_block): a rank's
+# longest payload on the head takes ~blocks x this / clock.
+CHAIN2_CYCLES_PER_BLOCK = 3319
+
+
+def c5_rank_summary(dist, world: int, form: str, *, n, nbytes, blocks, hashed, max_blocks, elapsed, kern_ms,
+                    clock_ghz, steps) -> dict:
+    """The N-rank c5 figures from each rank's own (every rank calls it): the job's
+    digests/s over the slowest rank's time, the roofline fraction of N GPUs' peak,
+    and, rank by rank, its kernel time, its longest payload and the estimated share
+    of its time that payload's serial chain takes on the two-lane head (the floor
+    of strong scaling: DESIGN.md (e)) -- so the driver's 8-GPU node shows which
+    rank and what bounds it."""
+    import torch
+    t = torch.tensor([elapsed, kern_ms], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed_max, kern_max = (float(x) for x in t.tolist())
+    tot = torch.tensor([n, nbytes, blocks, hashed], dtype=torch.float64)
+    dist.all_reduce(tot)
+    tn, tbytes, tblocks, thashed = (float(x) for x in tot.tolist())
+    mine = torch.tensor([kern_ms, float(max_blocks), float(clock_ghz or 0.0), float(n)], dtype=torch.float64)
+    every = [torch.zeros_like(mine) for _ in range(world)]
+    dist.all_gather(every, mine)
+    per_kern = [float(e[0]) for e in every]
+    per_max = [int(e[1]) for e in every]
+    per_clock = [float(e[2]) or PEAK_CLOCK_GHZ for e in every]
+    achieved = OPS_PER_BLOCK * thashed / (kern_max * 1e-3) / 1e12      # all GPUs, slowest rank's launch
+    out = {"form": C5_FORM_NOTES.get(form, form), "n_gpus": world, "scaling": "strong",
+           "value": tn * steps / elapsed_max, "unit": "digests/s",
+           "gbps_hashed": tbytes * steps / elapsed_max / 1e9, "ms_per_step": elapsed_max / steps * 1e3,
+           "kernel_ms_mean_max_over_ranks": kern_max,
+           "frac": achieved / (PEAK_VALU_TOPS * world), "achieved": achieved, "peak": PEAK_VALU_TOPS * world,
+           "blocks": int(tblocks), "hashed_blocks": int(thashed),
+           "effective_clock_ghz_rank0": clock_ghz,
+           "kernel_ms_per_rank": per_kern, "messages_per_rank": [int(e[3]) for e in every],
+           "max_blocks_per_rank": per_max}
+    if form in ("c5_planned", "c5_folded"):
+        est = [b * CHAIN2_CYCLES_PER_BLOCK / (c * 1e6) for b, c in zip(per_max, per_clock)]
+        out["head_chain_ms_est_per_rank"] = est
+        out["head_share_est_per_rank"] = [e / k if k > 0 else None for e, k in zip(est, per_kern)]
+        out["head_chain_note"] = ("a rank's longest payload on the two-lane head: max_blocks x %d cycles "
+                                  "(k_digest_chain2, PMC) / the rank's measured clock; share = that / the rank's "
+                                  "kernel_ms (near 1: the chain bounds the rank)" % CHAIN2_CYCLES_PER_BLOCK)
+    return out
 
 
 def run_lib(args):

@@ -109,3 +109,66 @@ def test_bench_two_ranks_on_the_engine():
     assert cb["cores"] == 1 and cb["value"] == cb["openssl"]["1_thread"]["value"] and cb["impl"]
     assert cb["scalar_port"]["value"] > 0
     assert d["host_api"]["first_launch_ms_max"] > 0
+
+
+def _summary_worker(rank, world, port, q):
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    out = {}
+    for form in bench.C5_FORMS:
+        # each rank's own figures, as extra_c5_ranks measures them on its GPU
+        out[form] = bench.c5_rank_summary(dist, world, form, n=1 << 20, nbytes=1 << 29, blocks=47_000_000 + rank,
+                                          hashed=8_000_000, max_blocks=1427 - rank, elapsed=0.02 + rank * 1e-3,
+                                          kern_ms=2.0 + rank * 0.01, clock_ghz=2.3, steps=10)
+    if rank == 0:
+        q.put(out)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_eight_rank_c5_line_reports_each_rank():
+    """a default bench line over 8 ranks (the driver's 8-GPU node)
+    carries, for c5_planned and c5_folded, every rank's kernel time, its longest
+    payload and the chain head's estimated share -- faked here with 8 gloo ranks on
+    the CPU (bench.c5_rank_summary is what extra_c5_ranks reports); and host_api
+    carries each GPU's upload rate (bench.host_api_summary)."""
+    import torch.multiprocessing as mp
+    import bench
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_summary_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=240)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for form in bench.C5_FORMS:
+        e = out[form]
+        assert e["n_gpus"] == world and len(e["kernel_ms_per_rank"]) == world
+        assert e["kernel_ms_per_rank"] == [2.0 + r * 0.01 for r in range(world)]
+        assert e["kernel_ms_mean_max_over_ranks"] == max(e["kernel_ms_per_rank"])
+        assert e["max_blocks_per_rank"] == [1427 - r for r in range(world)]
+        assert e["blocks"] == sum(47_000_000 + r for r in range(world))
+        if form == "c5":
+            assert "head_share_est_per_rank" not in e
+        else:
+            est = e["head_chain_ms_est_per_rank"]
+            assert len(est) == world and abs(est[0] - 1427 * bench.CHAIN2_CYCLES_PER_BLOCK / 2.3e6) < 1e-9
+            assert all(0 < s < 2 for s in e["head_share_est_per_rank"])
+    # host_api: per-GPU upload GB/s from a --mode lib line over 8 GPUs
+    shards = [{"device": g, "messages": 1 << 20, "lanes": 1 << 20, "head_lanes": 12, "h2d_bytes": 480e6,
+               "device_ms": 10.0, "upload_ms": 8.0 + g, "kernel_ms": 2.0, "first_launch_ms": 1.5,
+               "plan_kernel_ms": 0.2} for g in range(world)]
+    d = {"arena_bytes": 1, "value": 8e8, "n_gpus": world, "shards": world, "virtual_shards": None,
+         "ms_per_step": 11.0, "call_ms": [11.0], "gbps_hashed": 300.0, "steps": 5,
+         "last_call_stats": {"plan_ms": 1.5}, "last_call_shards": shards}
+    h = bench.host_api_summary(d, "test")
+    assert [g["upload_gbps"] for g in h["per_gpu"]] == [480e6 / (8.0 + g) / 1e6 for g in range(world)]
+    assert h["upload_gbps_min"] == 480e6 / 15.0 / 1e6 and h["upload_gbps_max"] == 60.0

@@ -1,0 +1,73 @@
+"""tools/pmc_summary.py publishes only valid derived figures: a
+kernel too short for GRBM_GUI_ACTIVE to resolve its clock gets clock_ghz null and
+a note (round 4 printed 6.01 GHz for k_fold_tilescan), and a step of several
+kernels, serialized under --pmc, reports serialized_frac over the serial sum and
+takes roofline_frac from the bench line's overlapped step. Synthetic counter
+files, CPU only."""
+import csv
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+KERNELS = [  # name, ns, GRBM_GUI_ACTIVE (summed over 8 XCDs), SQ_INSTS_VALU
+    ("void msha::k_digest_batch<2>(unsigned char const*)", 2_500_000, 8 * 2.3 * 2_500_000, 1.4e9),
+    ("msha::k_fold_tilescan(msha::FoldArgs, unsigned long)", 6_000, 8 * 6.01 * 6_000, 1e5),
+    ("msha::k_fold_insert(msha::FoldArgs)", 80_000, 8 * 2.9 * 80_000, 1e7),  # long enough, but > 2.6 GHz
+]
+
+
+def _write_pass(d, counters):
+    os.makedirs(d)
+    with open(os.path.join(d, "run_counter_collection.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
+        disp = 0
+        for step in range(3):
+            for name, ns, grbm, valu in KERNELS:
+                disp += 1
+                for c, v in counters(ns, grbm, valu).items():
+                    w.writerow([disp, name, c, v])
+    with open(os.path.join(d, "run_kernel_trace.csv"), "w", newline="") as f:
+        w = csv.writer(f)
+        w.writerow(["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
+        disp, t = 0, 1000
+        for step in range(3):
+            for name, ns, _, _ in KERNELS:
+                disp += 1
+                w.writerow([disp, name, t, t + ns])
+                t += ns + 1000
+
+
+def test_pmc_summary_publishes_only_valid_figures(tmp_path):
+    src = tmp_path / "pmc"
+    cfg = {"workload": "c5 synthetic", "blocks_per_gpu": 377_620_625, "messages_per_gpu": 8_388_608,
+           "hashed_blocks_per_gpu": 65_495_931, "max_blocks_per_message": 1427}
+    line = {"config": cfg, "roofline": {"algorithmic_bytes_per_launch": 1 << 30}}
+    _write_pass(str(src / "c5_folded_auto_sq"),
+                lambda ns, grbm, valu: {"GRBM_GUI_ACTIVE": grbm, "SQ_INSTS_VALU": valu,
+                                        "SQ_ACTIVE_INST_VALU": valu * 2, "SQ_WAVES": 1000,
+                                        "SQ_WAVE_CYCLES": 1e6, "SQ_WAIT_ANY": 1e4, "SQ_INSTS_SALU": 10})
+    (src / "c5_folded_auto_sq.log").write_text(json.dumps(line) + "\n")
+    bench = tmp_path / "bench_default.json"
+    bench.write_text(json.dumps({"extra_configs": {"c5_folded": {"roofline": {"frac": 0.421}}}}) + "\n")
+    dst = tmp_path / "out.json"
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pmc_summary.py"), str(src), str(dst), "",
+                        str(bench)], capture_output=True, text=True, cwd=ROOT)
+    assert r.returncode == 0, r.stderr
+    out = json.loads(dst.read_text())
+    c = out["configs"]["c5_folded_auto"]
+    ks = c["kernels"]
+    scan = ks["msha::k_fold_tilescan"]
+    assert scan["clock_ghz"] is None and scan["simd_cycles_per_valu_instr"] is None and "clock_note" in scan
+    ins = ks["msha::k_fold_insert"]
+    assert ins["clock_ghz"] is None and "clock_note" in ins
+    lane = ks["msha::k_digest_batch<2>"]
+    assert abs(lane["clock_ghz"] - 2.3) < 1e-6 and "clock_note" not in lane
+    for k in ks.values():
+        assert k["clock_ghz"] is None or k["clock_ghz"] <= 2.6
+    # several kernels: the serialized frac is over their sum, roofline_frac is the line's
+    assert c["roofline_frac"] == 0.421 and c["serialized_frac"] > 0
+    assert "roofline_frac_note" in c

@@ -6,7 +6,7 @@ VALUBusy, VALUUtilization), integer-op throughput against the int32 VALU peak,
 clock under load, and HBM bytes/GB/s (FETCH_SIZE x the gfx950 calibration +
 WRITE_SIZE).
 
-    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r04_pmc.json [calib.json]
+    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r05_pmc.json [calib.json] [bench_line.json]
 
 A bench step may run several kernels (the GPU-planned c5 forms: the k_fold_*
 planner, the head on k_digest_chain2 / k_digest_coop, the lane kernel, the alias
@@ -20,6 +20,17 @@ figures are exact, the step's kernel time is the serial sum.
 Top-level fields of a config describe its dominant hash kernel (the longest
 k_digest_*), as in earlier rounds' files, plus "kernels" (each kernel) and
 "step" (whole-step sums).
+
+Only valid derived figures are published (round 5):
+- clock_ghz (and the per-cycle figures built on it: SIMD cycles per VALU
+  instruction, VALUBusy) is null for a kernel shorter than MIN_CLOCK_US or when
+  it would exceed MAX_CLOCK_GHZ: GRBM_GUI_ACTIVE also counts the dispatch's ramp
+  and drain, which a 5-15 us kernel does not amortise (round 4 printed 6.01 GHz
+  for k_fold_tilescan); the entry says why in clock_note.
+- A step of several kernels runs them one after another under --pmc, so its
+  frac over the serial sum is "serialized_frac"; "roofline_frac" is the
+  overlapped step's, taken from a bench line (4th argument: a JSON line with
+  extra_configs, e.g. the round's default bench output), else null.
 """
 import csv
 import json
@@ -36,6 +47,9 @@ PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12
 SIMDS, CUS, XCDS = 1024, 256, 8
 HBM_PEAK_GBS = 8000.0
 TIMED = 3  # bench.py --steps 3 in tools/pmc_valu.sh
+MIN_CLOCK_US = 50.0   # below this, GRBM_GUI_ACTIVE / ns does not resolve the clock
+MAX_CLOCK_GHZ = 2.6   # MI355X's top clock is 2.4 GHz; more is a counter artefact
+BENCH = sys.argv[4] if len(sys.argv) > 4 else None
 # waves per workgroup of the kernels that hold a CU each (heads): the CUs they occupy
 WAVES_PER_WG = {"k_digest_chain2": 3, "k_digest_coop": 4}
 
@@ -119,11 +133,21 @@ def kernel_entry(k, sq, sq2, fe, wr, cf, max_blocks=0):
     active = mean(rows, "SQ_ACTIVE_INST_VALU")
     waves = mean(rows, "SQ_WAVES")
     wave_cyc = mean(rows, "SQ_WAVE_CYCLES")
-    e = {"us": ns / 1e3, "clock_ghz": cyc / ns if ns else None,
+    clk = cyc / ns if ns else None
+    note = None
+    if ns < MIN_CLOCK_US * 1e3:
+        note = ("kernel shorter than %g us: GRBM_GUI_ACTIVE spans the dispatch's ramp and drain, so the clock "
+                "and the per-cycle figures are not resolved" % MIN_CLOCK_US)
+    elif clk and clk > MAX_CLOCK_GHZ:
+        note = "counted clock %.2f GHz is above the part's %.1f GHz: not published" % (clk, 2.4)
+    ok = note is None
+    e = {"us": ns / 1e3, "clock_ghz": clk if ok else None,
          "valu_lane_instr": insts * 64, "salu_instr": mean(rows, "SQ_INSTS_SALU"), "waves": waves,
-         "simd_cycles_per_valu_instr": cyc * SIMDS / insts if insts else None,
-         "valu_busy_pct": 100 * active / CUS / cyc if cyc else None,
+         "simd_cycles_per_valu_instr": cyc * SIMDS / insts if insts and ok else None,
+         "valu_busy_pct": 100 * active / CUS / cyc if cyc and ok else None,
          "wait_any_share": mean(rows, "SQ_WAIT_ANY") / wave_cyc if wave_cyc else None}
+    if note:
+        e["clock_note"] = note
     base = k.split("<")[0].split("::")[-1]
     if base in WAVES_PER_WG and max_blocks:
         # a head: its time is its longest chain's (max_blocks blocks, serial);
@@ -145,8 +169,27 @@ def kernel_entry(k, sq, sq2, fe, wr, cf, max_blocks=0):
     return e
 
 
+def overlapped_fracs():
+    """{config: roofline.frac} of the bench line's extra_configs (and its headline),
+    measured with the step's kernels overlapped as they run in the bench."""
+    if not BENCH or not os.path.exists(BENCH):
+        return {}
+    with open(BENCH) as f:
+        lines = [l for l in f if l.lstrip().startswith("{")]
+    if not lines:
+        return {}
+    line = json.loads(lines[-1])
+    line = line.get("parsed", line) if "extra_configs" not in line else line
+    out = {}
+    for cfg, e in (line.get("extra_configs") or {}).items():
+        if isinstance(e, dict) and isinstance(e.get("roofline"), dict):
+            out[cfg] = e["roofline"].get("frac")
+    return out
+
+
 def main():
     cf, cf_src = calib_factor()
+    over = overlapped_fracs()
     names = sorted({d.rsplit("_", 1)[0] for d in os.listdir(SRC)
                     if os.path.isdir(os.path.join(SRC, d)) and d.endswith("_sq")})
     out = {"source": "tools/pmc_valu.sh (rocprofv3 --kernel-trace --pmc, one pass per counter group); "
@@ -162,7 +205,8 @@ def main():
                                          "(the head's time is that chain's)",
                "valu_utilization_pct": "VALUUtilization = 100 x SQ_THREAD_CYCLES_VALU / (SQ_ACTIVE_INST_VALU x 64)",
                "int32_share": "SQ_INSTS_VALU_INT32 / SQ_INSTS_VALU",
-               "algorithmic_tops": "1400 x hashed blocks / kernel ns (bench roofline.achieved); frac vs 78.64 T",
+               "algorithmic_tops": "1400 x hashed blocks / the step's serial kernel ns; serialized_frac vs 78.64 T",
+               "roofline_frac": "one-kernel steps: serialized_frac; several kernels: the bench line's overlapped frac",
                "hbm_bytes": "FETCH_SIZE x calib_factor (gfx950 half-count) + WRITE_SIZE, per kernel; the step's "
                             "is the sum over its kernels"},
            "configs": {}}
@@ -192,9 +236,17 @@ def main():
              "valu_busy_pct": d["valu_busy_pct"], "wait_any_share": d["wait_any_share"],
              "int32_share": d.get("int32_share"), "valu_utilization_pct": d.get("valu_utilization_pct"),
              "algorithmic_tops": OPS_PER_BLOCK * hashed / step_us / 1e6,
-             "roofline_frac": OPS_PER_BLOCK * hashed / step_us / 1e6 / PEAK_TOPS,
+             "serialized_frac": OPS_PER_BLOCK * hashed / step_us / 1e6 / PEAK_TOPS,
              "step": {"us_serialized": step_us, "kernels": sorted(kernels, key=lambda k: -kernels[k]["us"])},
              "kernels": kernels}
+        cfg_name = nm.rsplit("_", 1)[0]
+        if len(kernels) == 1:
+            e["roofline_frac"] = e["serialized_frac"]  # one kernel: nothing to overlap
+        else:
+            e["roofline_frac"] = over.get(cfg_name)
+            e["roofline_frac_note"] = ("the step's kernels overlap in the bench but run one after another under "
+                                       "--pmc: serialized_frac is over their serial sum; roofline_frac is the "
+                                       "bench line's (%s)" % (BENCH or "none given: null"))
         if probe:
             e["clock_probe_after_steps"] = next(iter(probe.values()))
         if all("hbm_bytes" in k for k in kernels.values()):
@@ -209,7 +261,8 @@ def main():
         print(f"{nm:20s} {e['kernel'][:34]:34s} {e['kernel_us']:9.1f} us step {e['step']['us_serialized']:9.1f}"
               f"  clk {e['clock_ghz'] or 0:.2f}  valu/blk {e['valu_instr_per_block']:7.0f}"
               f"  cyc/instr {e['simd_cycles_per_valu_instr'] or 0:.2f}  busy {e['valu_busy_pct'] or 0:5.1f}%"
-              f"  frac {e['roofline_frac']:.3f}  hbm x{e.get('hbm_over_algorithmic', 0):.2f}")
+              f"  frac {e['roofline_frac'] if e['roofline_frac'] is not None else float('nan'):.3f}"
+              f" (serialized {e['serialized_frac']:.3f})  hbm x{e.get('hbm_over_algorithmic', 0):.2f}")
         for k, v in e["kernels"].items():
             if k != e["kernel"]:
                 ch = v.get("cycles_per_chain_block")
