@@ -215,7 +215,7 @@ int msha_digest_batch_device(msha_ctx* ctx, const uint8_t* d_arena, const uint64
  * the launch (a mixed storm sharded over several GPUs), run on the cooperative
  * kernel beside the lane kernel (a side stream forked from and joined back to
  * `stream`). Same arena rules and error reporting as msha_digest_batch_device;
- * n < 2^32 - 1. Returns after enqueueing. Not capturable into a HIP graph: the
+ * n < 2^31. Returns after enqueueing. Not capturable into a HIP graph: the
  * call orders itself after the previous planned call through a library event
  * and forks to a library-owned stream, so on a capturing stream it fails with
  * MSHA_ERR_INVALID_ARG (msha_digest_batch_device captures).

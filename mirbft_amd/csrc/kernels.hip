@@ -198,25 +198,26 @@ __device__ __forceinline__ void hash_message_pipe(const uint8_t* p, uint64_t len
     expand_block(X, A);
     load_block16(blk(1), X);
     uint32_t b = 0;
-    auto take = [&](const uint32_t (&src)[16]) {
-#pragma unroll
-      for (int j = 0; j < 16; ++j) tail[j] = src[j];
-    };
+    // The tail block's bytes are loaded again after the loop (one 64-byte load a
+    // message) rather than taken from whichever raw buffer held them: with exit
+    // copies out of the rotating buffers the register allocator copied raw
+    // buffers inside the loop (8 v_mov a block).
     for (;;) {
       // A = schedule of block b (b % 4 == 0), X = bytes of block b+1 (clamped)
       load_block16(blk(b + 2), Y);
       load_block16(blk(b + 3), Z);
       rounds_expand(s, A, B, X);
-      if (++b >= nfull) { take(X); break; }
+      if (++b >= nfull) break;
       rounds_expand(s, B, A, Y);  // B = block b, Y = block b+1
-      if (++b >= nfull) { take(Y); break; }
+      if (++b >= nfull) break;
       load_block16(blk(b + 2), V);
       load_block16(blk(b + 3), X);
       rounds_expand(s, A, B, Z);  // A = block b, Z = block b+1
-      if (++b >= nfull) { take(Z); break; }
+      if (++b >= nfull) break;
       rounds_expand(s, B, A, V);  // B = block b, V = block b+1
-      if (++b >= nfull) { take(V); break; }
+      if (++b >= nfull) break;
     }
+    load_block16(blk(nfull), tail);
   }
   uint32_t w[16];
   for (uint32_t b = nfull; b < nvalu; ++b) {

@@ -114,8 +114,15 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t st);
 // kNoLane past the last; info[1] = the head of lanes whose chains would outlast
 // the lane kernel's throughput time, for the cooperative kernel (at most
 // head_cap). Block-count buckets: exact below 4,096 blocks, powers of two above.
+// Classes, ascending: a message shorter than kFoldExactLen bytes by its exact
+// length (a wave of one length hashes its padding block's schedule on the
+// scalar unit, kernels.hip compress_uniform_pad), then exact block counts in
+// [kFoldLowBlocks, 4096), then powers of two. Keys are descending classes.
+constexpr uint32_t kFoldExactLen = 1024;
+constexpr uint32_t kFoldLowBlocks = 16;   // (blocks of kFoldExactLen bytes: 17; 16 keeps the count even)
 constexpr uint32_t kFoldBigBuckets = 52;  // the power-of-two classes (>= 4,096 blocks): keys [0, 52)
-constexpr uint32_t kFoldBuckets = 4096 + kFoldBigBuckets;
+constexpr uint32_t kFoldBuckets = kFoldExactLen + (4096 - kFoldLowBlocks) + kFoldBigBuckets;
+static_assert(kFoldBuckets % 2 == 0, "FoldArgs::big follows the counters 8-byte aligned");
 struct FoldArgs {
   const uint64_t* off;
   const uint64_t* len;
@@ -123,14 +130,26 @@ struct FoldArgs {
   uint64_t* table = nullptr;  // tmask + 1 slots (epoch << 32 | message + 1); null: no folding
   uint64_t tmask = 0;
   uint32_t epoch = 1;         // this call's tag: a slot of another epoch is empty (never 0)
-  uint32_t* rep = nullptr;    // n (with table): the lane message i's digest comes from
+  // (with table) the folded messages, per tile of 4,096: apairs[tile * 4096 + k] =
+  // rep << 32 | i for k < acount[tile] -- message i's digest is message rep's
+  uint64_t* apairs = nullptr;
+  uint32_t* acount = nullptr;
   uint64_t* tmax = nullptr;   // (with table) ceil(n / 4096): largest offset before each tile
   uint64_t* tsum = nullptr;   // (early head) 2 per tile: the tile's short messages' blocks, its longest chain
-  uint32_t* cnt;              // kFoldBuckets zeroed counters -> bucket starts
+  uint32_t* cnt;              // kFoldBuckets zeroed counters (by key) -> bucket starts
   uint64_t* big = nullptr;    // 2 x kFoldBigBuckets zeroed: per power-of-two key, the largest
                               // block count and the block sum (the head's cost model needs the
                               // real longest chain, not the class's lower bound)
   uint32_t* order;            // n, kNoLane-filled -> position -> message index
+  uint16_t* key16 = nullptr;  // n: message i's key when it is a lane, else 0xFFFF (written by the
+                              // insert or the counts, read by the scatter instead of len and rep)
+  // Per tile of 4,096 messages, the keys its lanes hold and the tile's offset in
+  // each key's bucket, taken when the insert (or the counts) added its lanes to
+  // the bucket counters: tkeys[tile * 4096 + k] = key << 32 | offset for k <
+  // tkcount[tile]. The scatter places lanes at bucket start + offset + rank with
+  // no global atomics of its own.
+  uint64_t* tkeys = nullptr;
+  uint32_t* tkcount = nullptr;
   uint32_t* info;             // [0] lanes, [1] positions the lane kernel skips (the head's),
                               // [2] distinct long payloads, [3] k_fold_longs workgroups done,
                               // [4] the early head's lanes (0: none), [5] the late head's,
@@ -180,8 +199,8 @@ hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_a
 // The early head's list (FoldArgs::longs): on a stream of its own, after the
 // prefix, beside the alias insert (both claim through the same table).
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st);
-// out[i] = out[rep[i]] for every folded message (rep[i] != i), after the hashing.
-hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st);
+// out[i] = out[rep] for every folded message (FoldArgs::apairs), after the hashing.
+hipError_t launch_fold_fill(const FoldArgs& a, uint8_t* out, hipStream_t st);
 
 // Clock probe (msha_clock_probe): `workgroups` x 256 lanes compress `blocks`
 // register-resident blocks each; stamps gets (memtime, memrealtime) at start and

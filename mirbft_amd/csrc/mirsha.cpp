@@ -237,7 +237,7 @@ struct Device {
   // planned device calls (msha_digest_batch_device_planned): alias table,
   // representatives, bucket counters, lane order, [lanes | head]; the head of
   // long chains runs on side_stream, forked from and joined to the caller's
-  DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_info, f_longs;
+  DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_key, f_tkeys, f_longs;
   hipStream_t head_stream = nullptr;  // a folded call's early head (FoldArgs::longs)
   hipEvent_t ev_longs = nullptr, ev_join2 = nullptr;
   uint32_t f_epoch = 0;  // the alias table's epoch tag of the last folded call (plan.hip fold_claim)
@@ -269,7 +269,7 @@ struct Device {
     gather_pool.reset();
     for (DevBuf* b : {&arena, &off, &len, &order, &out, &err, &idx, &begin, &table, &sm_in, &sm_out, &p_meta,
                       &p_gmap, &p_devoff, &p_table, &p_slot, &p_rep, &p_cnt, &p_small, &f_table, &f_rep,
-                      &f_tmax, &f_cnt, &f_order, &f_info, &f_longs, &probe, &p_head})
+                      &f_tmax, &f_cnt, &f_order, &f_key, &f_tkeys, &f_longs, &probe, &p_head})
       b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
@@ -2715,7 +2715,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
 
   if (!d_arena || !d_off || !d_len || !d_out) return fail(ctx, MSHA_ERR_INVALID_ARG, "null pointer argument");
   if (flags & ~(uint32_t)MSHA_PLAN_FOLD_ALIASES) return fail(ctx, MSHA_ERR_INVALID_ARG, "unknown plan flags");
-  if (n >= msha::kNoLane) return fail(ctx, MSHA_ERR_INVALID_ARG, "planned device batches hold < 2^32 - 1 messages");
+  if (n >= (1ull << 31)) return fail(ctx, MSHA_ERR_INVALID_ARG, "planned device batches hold < 2^31 messages");
   return guarded(ctx, [&] {
     hipStream_t st;
     device_prologue(ctx, stream, &st);
@@ -2737,9 +2737,13 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     const bool head = !all_coop && ctx->kernel_policy != MSHA_KERNEL_LANE && env_u64("MSHA_PLAN_HEAD", 1) != 0;
     uint64_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
-    d.f_cnt.ensure(4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets);  // counters, then FoldArgs::big
+    // one zeroed block: info (12 words, padded to 64 bytes), the bucket counters,
+    // then FoldArgs::big -- cleared by ONE memset per call
+    const uint64_t fold_zero = 64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets;
+    d.f_cnt.ensure(fold_zero);
+    d.f_key.ensure(2 * n);
+    d.f_tkeys.ensure(8 * n + 4 * ((n + 4095) / 4096) + 8 * 4096);  // per-tile key lists, then their counts
     d.f_order.ensure(4 * n);
-    d.f_info.ensure(4 * 12);
     bool clear_table = false;
     if (fold) {
       // epoch-tagged slots (plan.hip fold_claim): cleared only when the table
@@ -2760,7 +2764,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
         d.f_epoch = 0;
       }
       ++d.f_epoch;
-      d.f_rep.ensure(4 * n);
+      d.f_rep.ensure(8 * n + 4 * ((n + 4095) / 4096));  // alias pairs, then their count per tile
       d.f_tmax.ensure(8 * 3 * ((n + 4095) / 4096));  // tile maxima, then 2 x tsum per tile
     }
     // The planner's scratch (table, order, counters) is the context's: a call
@@ -2784,8 +2788,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       ps = d.side_stream;
     }
     if (clear_table) HIPCHK(hipMemsetAsync(d.f_table.p, 0, d.f_table.cap, ps));
-    HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets, ps));
-    HIPCHK(hipMemsetAsync(d.f_info.p, 0, 4 * 12, ps));
+    HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, fold_zero, ps));
     // (the order's positions past the last lane are filled by k_fold_scatter)
     msha::FoldArgs fa;
     fa.off = d_off;
@@ -2795,13 +2798,17 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.table = fold ? d.f_table.as<uint64_t>() : nullptr;
     fa.tmask = cap - 1;
     fa.epoch = d.f_epoch;
-    fa.rep = fold ? d.f_rep.as<uint32_t>() : nullptr;
+    fa.apairs = fold ? d.f_rep.as<uint64_t>() : nullptr;
+    fa.acount = fold ? reinterpret_cast<uint32_t*>(fa.apairs + n) : nullptr;
     fa.tmax = fold ? d.f_tmax.as<uint64_t>() : nullptr;
     fa.tsum = fold ? fa.tmax + (n + 4095) / 4096 : nullptr;
-    fa.cnt = d.f_cnt.as<uint32_t>();
-    fa.big = reinterpret_cast<uint64_t*>(fa.cnt + msha::kFoldBuckets);  // 4 x 4,148 B: 8-byte aligned
+    fa.info = d.f_cnt.as<uint32_t>();
+    fa.cnt = fa.info + 16;
+    fa.key16 = d.f_key.as<uint16_t>();
+    fa.tkeys = d.f_tkeys.as<uint64_t>();
+    fa.tkcount = reinterpret_cast<uint32_t*>(fa.tkeys + (n + 4095) / 4096 * 4096);
+    fa.big = reinterpret_cast<uint64_t*>(fa.cnt + msha::kFoldBuckets);  // kFoldBuckets is even: 8-byte aligned
     fa.order = d.f_order.as<uint32_t>();
-    fa.info = d.f_info.as<uint32_t>();
     fa.simds = (uint32_t)d.cus * 4;
     // The head's kernel. Folded, a head is the few distinct long payloads: the
     // two-lane chain (k_digest_chain2, 64 messages per CU, ~10 % fewer cycles a
@@ -2884,7 +2891,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       if (head) HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
       if (early) HIPCHK(hipStreamWaitEvent(st, d.ev_join2, 0));
     }
-    if (fold) HIPCHK(msha::launch_fold_fill(fa.rep, n, d_out, st));
+    if (fold) HIPCHK(msha::launch_fold_fill(fa, d_out, st));
     HIPCHK(hipEventRecord(d.ev_fdone, st));
     d.fdone_recorded = true;
     ctx->stats.planned_device_calls++;

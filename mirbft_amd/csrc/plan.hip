@@ -294,15 +294,24 @@ hipError_t launch_plan(const PlanArgs& a, hipStream_t st) {
 //                   lane kernel would outlast the launch's floor (FoldArgs)
 //   k_fold_scatter  order[position] = message; kNoLane past the last lane
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint32_t fold_bucket(uint64_t blocks) {  // ascending class
-  if (blocks < 4096) return (uint32_t)blocks;
-  return 4096u + (uint32_t)(63 - __clzll((long long)blocks)) - 12u;
+// Ascending class of a message (kernels.hpp kFoldExactLen): exact length below
+// 1 KiB, so a wave of lanes sorted together holds one length -- round 4 keyed by
+// block count alone, and a 9-block bucket mixing 512-byte requests with 544-byte
+// Batches left most of folded c5's request waves with two lengths, off the
+// scalar-unit padding path (c2's 1,356 VALU instructions a block against ~1,400).
+__device__ __forceinline__ uint32_t fold_class(uint64_t len) {
+  if (len < kFoldExactLen) return (uint32_t)len;
+  const uint64_t blocks = dev_blocks_for(len);
+  if (blocks < 4096) return kFoldExactLen + (uint32_t)(blocks - kFoldLowBlocks);
+  return kFoldExactLen + (4096 - kFoldLowBlocks) + (uint32_t)(63 - __clzll((long long)blocks)) - 12u;
 }
-__device__ __forceinline__ uint64_t fold_bucket_blocks(uint32_t b) {  // lower bound
-  return b < 4096 ? b : (1ull << (b - 4096 + 12));
+__device__ __forceinline__ uint64_t fold_class_blocks(uint32_t c) {  // exact, or the lower bound (big classes)
+  if (c < kFoldExactLen) return dev_blocks_for(c);
+  if (c < kFoldExactLen + (4096 - kFoldLowBlocks)) return c - kFoldExactLen + kFoldLowBlocks;
+  return 1ull << (c - (kFoldExactLen + (4096 - kFoldLowBlocks)) + 12);
 }
-__device__ __forceinline__ uint32_t fold_key(uint64_t len) {  // descending block count
-  return kFoldBuckets - 1 - fold_bucket(dev_blocks_for(len));
+__device__ __forceinline__ uint32_t fold_key(uint64_t len) {  // descending class
+  return kFoldBuckets - 1 - fold_class(len);
 }
 
 // Candidates first (the host path's rule, msha_alias_first): a message whose
@@ -473,7 +482,7 @@ __device__ __forceinline__ void fold_hist_big(FoldHist& h, uint32_t k, uint64_t 
 }
 __device__ __forceinline__ void fold_hist_add(FoldHist& h, uint64_t len) {
   const uint64_t blocks = dev_blocks_for(len);
-  const uint32_t k = kFoldBuckets - 1 - fold_bucket(blocks);
+  const uint32_t k = fold_key(len);
   atomicAdd(&h.n[k], 1u);
   fold_hist_big(h, k, blocks);
 }
@@ -482,7 +491,7 @@ __device__ __forceinline__ void fold_hist_add(FoldHist& h, uint64_t len) {
 // which one LDS atomic per lane serialises ~45 deep), the rest one each.
 __device__ __forceinline__ void fold_hist_add_wave(FoldHist& h, bool valid, uint64_t len) {
   const uint64_t blocks = dev_blocks_for(len);
-  const uint32_t k = valid ? kFoldBuckets - 1 - fold_bucket(blocks) : 0xFFFFFFFFu;
+  const uint32_t k = valid ? fold_key(len) : 0xFFFFFFFFu;
   const uint64_t any = __ballot(valid);
   if (!any) return;
   const uint32_t k0 = __shfl(k, __ffsll((long long)any) - 1);
@@ -495,13 +504,23 @@ __device__ __forceinline__ void fold_hist_add_wave(FoldHist& h, bool valid, uint
   }
   if (valid) fold_hist_big(h, k, blocks);
 }
-__device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h) {
+// Each key present in the tile: one global atomic, whose return is the tile's
+// offset in the key's bucket, kept in the tile's key list (FoldArgs::tkeys) for
+// the scatter. nk: an LDS counter the caller zeroed before a barrier; every
+// thread of the workgroup calls this.
+__device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h, uint32_t& nk) {
+  uint64_t* tl = a.tkeys + (uint64_t)blockIdx.x * kPlanTile;
   for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
-    if (h.n[j]) atomicAdd(&a.cnt[j], h.n[j]);
+    if (h.n[j]) {
+      const uint32_t off = atomicAdd(&a.cnt[j], h.n[j]);
+      tl[atomicAdd(&nk, 1u)] = ((uint64_t)j << 32) | off;
+    }
   if (threadIdx.x < kFoldBigBuckets && h.bsum[threadIdx.x]) {
     atomicMax(reinterpret_cast<unsigned long long*>(&a.big[threadIdx.x]), h.bmax[threadIdx.x]);
     atomicAdd(reinterpret_cast<unsigned long long*>(&a.big[kFoldBigBuckets + threadIdx.x]), h.bsum[threadIdx.x]);
   }
+  __syncthreads();
+  if (threadIdx.x == 0) a.tkcount[blockIdx.x] = nk;
 }
 
 // Also counts the tile's lanes into the bucket histogram (what k_fold_keys
@@ -512,14 +531,17 @@ __device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h) 
 // words of consecutive messages per wave instruction (whole lines, not 4 bytes
 // per lane at a 64-byte stride), and the candidates' list is appended and the
 // histogram counted wave-aggregated.
+constexpr uint32_t kLaneMark = 0x80000000u;
 __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   __shared__ uint64_t part[256];
   __shared__ FoldHist hist;
-  __shared__ uint32_t trep[kPlanTile];   // the tile's representatives, by position in the tile
+  // the tile's representatives by position, a lane's as kLaneMark | its key
+  // (planned batches hold < 2^31 messages, mirsha.cpp: no index has that bit)
+  __shared__ uint32_t trep[kPlanTile];
   __shared__ uint16_t cand[kPlanTile];   // candidates' positions in the tile
-  __shared__ uint32_t ncand;
+  __shared__ uint32_t ncand, nalias, nkeys;
   fold_hist_clear(hist);
-  if (threadIdx.x == 0) ncand = 0;
+  if (threadIdx.x == 0) ncand = nalias = nkeys = 0;
   const uint64_t tile0 = (uint64_t)blockIdx.x * kPlanTile;
   const uint32_t lb = threadIdx.x * kPlanItems;
   const uint64_t base = tile0 + lb;
@@ -553,7 +575,7 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     const bool lng = valid && a.long_blocks && dev_blocks_for(l[r]) >= a.long_blocks;
     const bool fresh = valid && !lng && (o[r] > run || (first_ever && r == 0));
     const bool is_cand = valid && !fresh;
-    if (fresh) trep[lb + r] = (uint32_t)i;
+    if (fresh) trep[lb + r] = kLaneMark | fold_key(l[r]);
     fold_hist_add_wave(hist, fresh, l[r]);
     const uint64_t cm = __ballot(is_cand);
     if (cm) {
@@ -571,16 +593,33 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     const uint64_t i = tile0 + li;
     const uint64_t ln = a.len[i];
     const uint32_t rp = fold_claim(a, i, a.off[i], ln);
-    trep[li] = rp;
+    trep[li] = rp == (uint32_t)i ? kLaneMark | fold_key(ln) : rp;
     if (rp == (uint32_t)i) fold_hist_add(hist, ln);
   }
   __syncthreads();
+  // lane keys out, consecutive messages per wave instruction; the folded messages
+  // as (rep, i) pairs into the tile's segment of apairs, so the fill reads only
+  // them (c5: 5 % of the messages) instead of a representative per message
 #pragma unroll 4
   for (uint32_t r = 0; r < kPlanItems; ++r) {
     const uint32_t li = r * 256 + threadIdx.x;
-    if (tile0 + li < a.n) a.rep[tile0 + li] = trep[li];
+    const uint64_t i = tile0 + li;
+    const bool valid = i < a.n;
+    const uint32_t v = valid ? trep[li] : 0u;
+    const bool lane_i = v & kLaneMark;
+    if (valid) a.key16[i] = lane_i ? (uint16_t)(v & 0xFFFFu) : (uint16_t)0xFFFFu;
+    const bool folded = valid && !lane_i;
+    const uint64_t fm = __ballot(folded);
+    if (fm) {
+      uint32_t at = 0;
+      const int leader = __ffsll((long long)fm) - 1;
+      if ((int)lane == leader) at = atomicAdd(&nalias, (uint32_t)__popcll(fm));
+      at = __shfl(at, leader);
+      if (folded) a.apairs[tile0 + at + (uint32_t)__popcll(fm & ((1ull << lane) - 1))] = ((uint64_t)v << 32) | (uint32_t)i;
+    }
   }
-  fold_hist_flush(a, hist);
+  fold_hist_flush(a, hist, nkeys);  // (its barrier also completes nalias)
+  if (threadIdx.x == 0) a.acount[blockIdx.x] = nalias;
 }
 
 // The fold planner's keys are few (kFoldBuckets), so a tile counts them in a
@@ -590,30 +629,37 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
 // 210-270 us per pass, latency-bound).
 constexpr uint32_t kFoldItems = kPlanItems;          // messages per thread
 constexpr uint32_t kFoldTile = 256 * kFoldItems;     // messages per workgroup
-static_assert(kFoldTile <= 4096 && (kFoldBuckets << 12) < kEmptyKey, "scatter packs key << 12 | rank");
+static_assert(kFoldTile == kPlanTile, "the insert, the counts and the scatter share one tiling (tkeys, apairs)");
+static_assert(kFoldBuckets < 0xFFFFu, "keys fit key16 below its no-lane mark");
 
 // Without folding every message is a lane (with folding k_fold_insert counts).
 __global__ __launch_bounds__(256) void k_fold_keys(FoldArgs a) {
   __shared__ FoldHist hist;
+  __shared__ uint32_t nkeys;
   fold_hist_clear(hist);
+  if (threadIdx.x == 0) nkeys = 0;
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
 #pragma unroll 4
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    if (i < a.n) fold_hist_add(hist, a.len[i]);
+    if (i < a.n) {
+      const uint64_t l = a.len[i];
+      fold_hist_add(hist, l);
+      a.key16[i] = (uint16_t)fold_key(l);
+    }
   }
   __syncthreads();
-  fold_hist_flush(a, hist);
+  fold_hist_flush(a, hist, nkeys);
 }
 
 // Key k's longest chain and its c lanes' blocks: exact below 4,096 blocks (one
 // class per count), measured by k_fold_keys for the power-of-two classes above.
 __device__ __forceinline__ uint64_t key_max_blocks(const FoldArgs& a, uint32_t k) {
-  return k < kFoldBigBuckets ? a.big[k] : fold_bucket_blocks(kFoldBuckets - 1 - k);
+  return k < kFoldBigBuckets ? a.big[k] : fold_class_blocks(kFoldBuckets - 1 - k);
 }
 __device__ __forceinline__ uint64_t key_sum_blocks(const FoldArgs& a, uint32_t k, uint32_t c) {
-  return k < kFoldBigBuckets ? a.big[kFoldBigBuckets + k] : (uint64_t)c * fold_bucket_blocks(kFoldBuckets - 1 - k);
+  return k < kFoldBigBuckets ? a.big[kFoldBigBuckets + k] : (uint64_t)c * fold_class_blocks(kFoldBuckets - 1 - k);
 }
 
 // The head. Per candidate cut k (lanes with keys below k -- the longest -- go
@@ -740,31 +786,26 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   }
 }
 
-// Each lane's rank inside its tile's key (LDS atomic), the tile's base in
-// each bucket (one global atomic per key present), order[base + rank] = i.
+// Each lane's position: its key's bucket start, plus its tile's offset in the
+// bucket (taken by the insert or the counts, FoldArgs::tkeys), plus its rank
+// inside the tile (LDS atomic); order[position] = i. No global atomics: round 4
+// took each tile's offsets here, 2,048 tiles' returning atomics on the few hot
+// keys of a storm.
 __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
-  __shared__ uint32_t hist[kFoldBuckets];  // counts, then the tile's bucket bases
-  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x) hist[j] = 0;
+  __shared__ uint32_t pos[kFoldBuckets];  // next position of each key the tile holds
+  const uint32_t nk = a.tkcount[blockIdx.x];
+  const uint64_t* tl = a.tkeys + (uint64_t)blockIdx.x * kPlanTile;
+  for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) {
+    const uint64_t v = tl[k];
+    pos[v >> 32] = a.cnt[v >> 32] + (uint32_t)v;  // bucket start (k_fold_scan) + the tile's offset
+  }
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
-  uint32_t item[kFoldItems];  // key << 12 | rank (rank < kFoldTile = 4096), or kEmptyKey
 #pragma unroll
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    item[r] = kEmptyKey;
-    if (i < a.n && (!a.table || a.rep[i] == (uint32_t)i)) {
-      const uint32_t k = fold_key(a.len[i]);
-      item[r] = (k << 12) | atomicAdd(&hist[k], 1u);
-    }
-  }
-  __syncthreads();
-  for (uint32_t j = threadIdx.x; j < kFoldBuckets; j += blockDim.x)
-    if (hist[j]) hist[j] = atomicAdd(&a.cnt[j], hist[j]);
-  __syncthreads();
-#pragma unroll
-  for (uint32_t r = 0; r < kFoldItems; ++r) {
-    if (item[r] == kEmptyKey) continue;
-    a.order[hist[item[r] >> 12] + (item[r] & 0xFFFu)] = (uint32_t)(base + r * 256 + threadIdx.x);
+    const uint32_t k = i < a.n ? a.key16[i] : 0xFFFFu;
+    if (k != 0xFFFFu) a.order[atomicAdd(&pos[k], 1u)] = (uint32_t)i;
   }
   // positions past the last lane (the folded aliases' share) hold kNoLane
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -861,16 +902,18 @@ hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
   return hipGetLastError();
 }
 
-__global__ __launch_bounds__(256) void k_fold_fill(const uint32_t* __restrict__ rep, uint64_t n,
-                                                   uint8_t* __restrict__ out) {
-  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const uint32_t r = rep[i];
-  if (r == (uint32_t)i) return;
-  const uint4* src = reinterpret_cast<const uint4*>(out + 32 * (uint64_t)r);
-  uint4* dst = reinterpret_cast<uint4*>(out + 32 * i);
-  dst[0] = src[0];
-  dst[1] = src[1];
+// One workgroup per insert tile: its folded messages copy their representative's
+// digest (32 bytes each).
+__global__ __launch_bounds__(256) void k_fold_fill(FoldArgs a, uint8_t* __restrict__ out) {
+  const uint32_t cnt = a.acount[blockIdx.x];
+  const uint64_t* p = a.apairs + (uint64_t)blockIdx.x * kPlanTile;
+  for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+    const uint64_t v = p[k];
+    const uint4* src = reinterpret_cast<const uint4*>(out + 32 * (v >> 32));
+    uint4* dst = reinterpret_cast<uint4*>(out + 32 * (v & 0xFFFFFFFFull));
+    dst[0] = src[0];
+    dst[1] = src[1];
+  }
 }
 
 hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st) {
@@ -896,9 +939,9 @@ hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_a
   return hipGetLastError();
 }
 
-hipError_t launch_fold_fill(const uint32_t* rep, uint64_t n, uint8_t* out, hipStream_t st) {
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fold_fill, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, rep, n, out);
+hipError_t launch_fold_fill(const FoldArgs& a, uint8_t* out, hipStream_t st) {
+  if (a.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_fold_fill, dim3((unsigned)((a.n + kPlanTile - 1) / kPlanTile)), dim3(256), 0, st, a, out);
   return hipGetLastError();
 }
 

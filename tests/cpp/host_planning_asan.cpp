@@ -35,7 +35,7 @@ hipError_t launch_plan(const PlanArgs&, hipStream_t) { abort(); }
 hipError_t launch_fold_prefix(const FoldArgs&, hipStream_t) { abort(); }
 hipError_t launch_fold_plan(const FoldArgs&, hipStream_t, hipEvent_t) { abort(); }
 hipError_t launch_fold_longs(const FoldArgs&, int, hipStream_t) { abort(); }
-hipError_t launch_fold_fill(const uint32_t*, uint64_t, uint8_t*, hipStream_t) { abort(); }
+hipError_t launch_fold_fill(const FoldArgs&, uint8_t*, hipStream_t) { abort(); }
 hipError_t launch_clock_probe(uint32_t, uint32_t, uint64_t*, uint32_t*, hipStream_t) { abort(); }
 bool uses_coop(uint64_t, int, int) { abort(); }
 }  // namespace msha

@@ -13,6 +13,11 @@
 //   new10u: new10 with the kh DPP unmasked (bank_mask 0xf)
 //   old11+lds / old11+lds_e: old11 with a ds_read_b128 every 4 rounds (all lanes / e-lanes)
 //   xad10+nop: kh by v_xad_u32 (no DPP), both mirror DPPs W = mirror(W) + u, s_nop 0 between
+//   oct10 : round 5's candidate for VERDICT r4 #3, eight lanes a message -- each
+//           lane ONE rotate (e-quad: 6/11/25, a-quad: 2/13/22), Sigma by two
+//           quad_perm DPP xors, Ch and Maj, h + K+W, T1 by add3, T2, then e' and
+//           a' by two DPP adds across the quads (row_ror:4 / row_ror:12, bank
+//           masks): 10 instructions, 4 of them DPP
 // Build: hipcc --offload-arch=gfx950 -O3 -o tools/round_issue_microbench tools/round_issue_microbench.hip
 #include <hip/hip_runtime.h>
 
@@ -74,6 +79,17 @@ constexpr int kIters = 2048;
   "v_xad_u32 %[kh], %[" #Z "], %[M], %[k]\n\t"                                          \
   "s_nop 0\n\t"                                                                        \
   "v_add_u32_dpp %[" #W "], %[" #W "], %[u] row_mirror row_mask:0xf bank_mask:0xc\n\t"
+#define R_OCT(X, Y, Z, W)                                                                  \
+  "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh1]\n\t"                                 \
+  "v_bitop3_b32 %[c], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xca\n\t"                     \
+  "v_bitop3_b32 %[m], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xe8\n\t"                     \
+  "v_xor_b32_dpp %[s2], %[s1], %[s1] quad_perm:[1,2,0,3] row_mask:0xf bank_mask:0xf\n\t"   \
+  "v_add_u32 %[sk], %[" #W "], %[k]\n\t"                                                    \
+  "v_xor_b32_dpp %[s], %[s1], %[s2] quad_perm:[2,0,1,3] row_mask:0xf bank_mask:0xf\n\t"    \
+  "v_add3_u32 %[u], %[s], %[c], %[sk]\n\t"                                                  \
+  "v_add_u32 %[t], %[s], %[m]\n\t"                                                          \
+  "v_add_u32_dpp %[" #W "], %[" #W "], %[u] row_ror:4 row_mask:0xf bank_mask:0x5\n\t"      \
+  "v_add_u32_dpp %[" #W "], %[u], %[t] row_ror:12 row_mask:0xf bank_mask:0xa\n\t"
 #define KH_DPPU(Z) "v_add_u32_dpp %[kh], %[" #Z "], %[k] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0xf\n\t"
 #define KH_DPP(Z) "v_add_u32_dpp %[kh], %[" #Z "], %[k] quad_perm:[0,1,2,3] row_mask:0xf bank_mask:0x3\n\t"
 #define KH_VALU(Z) "v_add_u32 %[kh], %[" #Z "], %[k]\n\t"
@@ -161,6 +177,7 @@ __global__ __launch_bounds__(64) void k_rounds(uint32_t* out, uint64_t* ticks) {
       asm volatile(FOURL(R_OLD, LDSA) FOURL(R_OLD, LDSA) FOURL(R_OLD, LDSA) FOURL(R_OLD, LDSA) "s_waitcnt lgkmcnt(0)\n\t" OPSL);
     if (V == 10)
       asm volatile(FOURL(R_OLD, LDSE) FOURL(R_OLD, LDSE) FOURL(R_OLD, LDSE) FOURL(R_OLD, LDSE) "s_waitcnt lgkmcnt(0)\n\t" OPSL);
+    if (V == 11) asm volatile(FOUR(R_OCT) FOUR(R_OCT) FOUR(R_OCT) FOUR(R_OCT) OPS);
   }
   const uint64_t t1 = __builtin_amdgcn_s_memtime();
   out[lane] = X ^ Y ^ Z ^ W ^ kh ^ s1 ^ s2 ^ s3 ^ s ^ sk ^ c ^ u ^ m ^ t ^ q.x ^ q.w;
@@ -186,13 +203,13 @@ int main() {
   uint64_t* ticks;
   CHECK(hipMalloc(&out, 64 * 4));
   CHECK(hipMalloc(&ticks, 8));
-  const char* names[] = {"old11", "new10", "new10v", "valu11", "dpp8", "valu8", "new10b", "new10u", "xad10+nop", "old11+lds", "old11+lds_e"};
-  const int instrs[] = {11, 10, 10, 11, 8, 8, 10, 10, 11, 11, 11};
-  double r[11] = {run<0>(out, ticks), run<1>(out, ticks), run<2>(out, ticks),
+  const char* names[] = {"old11", "new10", "new10v", "valu11", "dpp8", "valu8", "new10b", "new10u", "xad10+nop", "old11+lds", "old11+lds_e", "oct10"};
+  const int instrs[] = {11, 10, 10, 11, 8, 8, 10, 10, 11, 11, 11, 10};
+  double r[12] = {run<0>(out, ticks), run<1>(out, ticks), run<2>(out, ticks),
                  run<3>(out, ticks), run<4>(out, ticks), run<5>(out, ticks),
                  run<6>(out, ticks), run<7>(out, ticks), run<8>(out, ticks),
-                 run<9>(out, ticks), run<10>(out, ticks)};
-  for (int v = 0; v < 11; ++v)
+                 run<9>(out, ticks), run<10>(out, ticks), run<11>(out, ticks)};
+  for (int v = 0; v < 12; ++v)
     printf("{\"variant\": \"%s\", \"instr_per_round\": %d, \"ticks_per_round\": %.2f, \"ticks_per_instr\": %.3f}\n",
            names[v], instrs[v], r[v], r[v] / instrs[v]);
   return 0;
