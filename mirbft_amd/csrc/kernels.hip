@@ -1217,6 +1217,217 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
     }
   }
 }
+
+// ---------------------------------------------------------------------------
+// Eight lanes a message (round 5; VERDICT r4 #3: the chain that bounds c5 over 8
+// GPUs). The two-lane round spends 3 of its 11 instructions on the three
+// rotations of Sigma, one after another in each lane. Here a message is two
+// quads -- the e-side (e f g h) in lanes 0-3 and the a-side (a b c d) in lanes
+// 4-7 of its 8 -- and each lane makes ONE rotation of its side's word (e: 6,
+// 11, 25, 6; a: 2, 13, 22, 2), the quad's three then XORed by two quad_perm
+// DPP xors that leave Sigma in all four lanes; Ch and Maj one bitop3 each; the
+// two new words by two DPP adds across the quads (row_ror:12 reads the a-quad
+// four lanes up, row_ror:4 the e-quad four down; bank_mask writes one side).
+// 10 instructions a round, 4 of them DPP: 41.4 shader cycles a round on a lone
+// wave against 45.4 for the two-lane round (tools/round_issue_microbench.hip
+// oct10, profiles/r05_chain/). Every lane of a quad holds its side's whole
+// state, so nothing is broadcast.
+//  E-round: s1 = rot, c = Ch, m = Maj, s2 = s1 ^ qp[1,0,3,1](s1), sk = W + K
+//    (h + K+W in the e-quad), s = s2 ^ qp[2,2,1,2](s1), u = s + c + sk (T1),
+//    t = s + m (T2 in the a-quad), e' = ror12(W) + u (d from the a-quad),
+//    a' = ror4(u) + t (T1 from the e-quad).
+//  A-round: y = W + K first (d + K+W in the a-quad), ..., u = s + c + W
+//    (Sigma1 + Ch + h), t = s + m + K (T2 + K+W), e' = ror12(y) + u, a' = ror4(u) + t.
+// K+W exactly as the two-lane kernel's form 4 (the e-quad reads the even
+// rounds' quad, the a-quad the odd rounds'): the same producer, one
+// ds_read_b128 per lane per 8 rounds. DPP sources read here are written >= 2
+// instructions earlier (tools/check_dpp_hazards.py checks the built library).
+// A consumer wave is 8 messages and each consumer owns a SIMD: 3 consumer waves
+// and the producer a workgroup, 24 messages a CU (the two-lane kernel: 64) --
+// a latency kernel for the few long payloads of a folded head.
+// ---------------------------------------------------------------------------
+#define MSHA_ASM_E8(X, Y, Z, W, K)                                                               \
+  "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh]\n\t"                                        \
+  "v_bitop3_b32 %[c], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xca\n\t"                           \
+  "v_bitop3_b32 %[m], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xe8\n\t"                           \
+  "v_xor_b32_dpp %[s2], %[s1], %[s1] quad_perm:[1,0,3,1] row_mask:0xf bank_mask:0xf\n\t"         \
+  "v_add_u32 %[sk], %[" #W "], %[" #K "]\n\t"                                                     \
+  "v_xor_b32_dpp %[s], %[s1], %[s2] quad_perm:[2,2,1,2] row_mask:0xf bank_mask:0xf\n\t"          \
+  "v_add3_u32 %[u], %[s], %[c], %[sk]\n\t"                                                        \
+  "v_add_u32 %[t], %[s], %[m]\n\t"                                                                \
+  "v_add_u32_dpp %[" #W "], %[" #W "], %[u] row_ror:12 row_mask:0xf bank_mask:0x5\n\t"           \
+  "v_add_u32_dpp %[" #W "], %[u], %[t] row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
+#define MSHA_ASM_A8(X, Y, Z, W, K)                                                               \
+  "v_add_u32 %[y], %[" #W "], %[" #K "]\n\t"                                                      \
+  "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh]\n\t"                                        \
+  "v_bitop3_b32 %[c], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xca\n\t"                           \
+  "v_bitop3_b32 %[m], %[" #X "], %[" #Y "], %[" #Z "] bitop3:0xe8\n\t"                           \
+  "v_xor_b32_dpp %[s2], %[s1], %[s1] quad_perm:[1,0,3,1] row_mask:0xf bank_mask:0xf\n\t"         \
+  "v_xor_b32_dpp %[s], %[s1], %[s2] quad_perm:[2,2,1,2] row_mask:0xf bank_mask:0xf\n\t"          \
+  "v_add3_u32 %[u], %[s], %[c], %[" #W "]\n\t"                                                    \
+  "v_add3_u32 %[t], %[s], %[m], %[" #K "]\n\t"                                                    \
+  "v_add_u32_dpp %[" #W "], %[y], %[u] row_ror:12 row_mask:0xf bank_mask:0x5\n\t"                \
+  "v_add_u32_dpp %[" #W "], %[u], %[t] row_ror:4 row_mask:0xf bank_mask:0xa\n\t"
+#define MSHA_ASM8_OPERANDS                                                                       \
+  : [X] "+v"(X), [Y] "+v"(Y), [Z] "+v"(Z), [W] "+v"(W), [s1] "=&v"(s1_), [s2] "=&v"(s2_),      \
+    [s] "=&v"(s_), [sk] "=&v"(sk_), [c] "=&v"(c_), [u] "=&v"(u_), [m] "=&v"(m_), [t] "=&v"(t_),  \
+    [y] "=&v"(y_)                                                                                \
+  : [sh] "v"(sh), [k0] "v"(v_.x), [k1] "v"(v_.y), [k2] "v"(v_.z), [k3] "v"(v_.w)
+#define MSHA_DQ8(cur, nxt, q)                                                                    \
+  {                                                                                              \
+    const uint4 v_ = cur[q];                                                                     \
+    nxt[q] = nk[col + (q) * 128];                                                                \
+    uint32_t s1_, s2_, s_, sk_, c_, u_, m_, t_, y_;                                              \
+    asm volatile(MSHA_ASM_E8(X, Y, Z, W, k0) MSHA_ASM_A8(W, X, Y, Z, k0)                         \
+                 MSHA_ASM_E8(Z, W, X, Y, k1) MSHA_ASM_A8(Y, Z, W, X, k1)                         \
+                 MSHA_ASM_E8(X, Y, Z, W, k2) MSHA_ASM_A8(W, X, Y, Z, k2)                         \
+                 MSHA_ASM_E8(Z, W, X, Y, k3) MSHA_ASM_A8(Y, Z, W, X, k3)                         \
+                 MSHA_ASM8_OPERANDS);                                                            \
+  }
+#define MSHA_DBLOCK8(cur, nxt)                                                                   \
+  {                                                                                              \
+    uint32_t X = H0, Y = H1, Z = H2, W = H3;                                                     \
+    _Pragma("unroll") for (int q_ = 0; q_ < 8; ++q_) MSHA_DQ8(cur, nxt, q_)                      \
+    H0 += X; H1 += Y; H2 += Z; H3 += W;                                                          \
+    if (active && sub == 0 && b + 1 == nb)                                                       \
+      *reinterpret_cast<uint4*>(out + 32 * o + (eside ? 16 : 0)) =                               \
+          make_uint4(bswap(H0), bswap(H1), bswap(H2), bswap(H3));                                \
+  }
+
+template <int MODE, bool EXCL>
+__global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint64_t* __restrict__ len,
+                                                       const uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ out_idx,
+                                                       uint64_t n, uint8_t* __restrict__ out,
+                                                       uint32_t* __restrict__ err,
+                                                       const uint32_t* __restrict__ limit) {
+  static_assert(MSHA_CHAIN2_FORM == 4, "the eight-lane rounds read form 4's K+W layout");
+  __shared__ uint4 kw[2][kC2Per][kCoopSlotQuads * 64];
+  __shared__ uint32_t s_nb;
+  if (EXCL) asm volatile("" ::: "v255", "a255");  // exclusive CU (see k_digest_coop EXCL)
+  if (EXCL) __builtin_amdgcn_s_setprio(3);
+  const unsigned lane = threadIdx.x & 63;
+  const unsigned wave = threadIdx.x >> 6;
+  const bool producer = wave == 0;
+  const bool eside = (lane & 4) == 0;
+  const unsigned sub = lane & 3;
+  // message of this lane inside the workgroup: the producer's lanes 0-23, each
+  // consumer wave's 8 (8 lanes each)
+  const unsigned msg = producer ? lane : (wave - 1) * 8 + (lane >> 3);
+  const uint64_t i = (uint64_t)blockIdx.x * kChain8MsgsPerWg + msg;
+  bool active = msg < kChain8MsgsPerWg && i < n && (!limit || i < *limit);
+  uint64_t m = i;  // metadata index
+  if (active && order) {
+    const uint32_t v = order[i];
+    active = v != kNoLane;
+    m = v;
+  }
+  uint64_t o = m;  // digest slot
+  if (active && out_idx) o = out_idx[i];
+  if (!active) m = o = 0;
+  const uint8_t* pa = arena;
+  uint64_t L = 0;
+  if (active) {
+    pa = arena + off[m];
+    L = len[m];
+    if (reinterpret_cast<uintptr_t>(pa) & 15) {
+      active = false;
+      L = 0;
+      if (!producer && eside && sub == 0) check_aligned(pa, out + 32 * o, err);
+    }
+  }
+  const uint32_t nfull = (uint32_t)(L >> 6), r = (uint32_t)(L & 63);
+  const uint32_t nb = nfull + (r < 56 ? 1 : 2);
+  if (threadIdx.x == 0) s_nb = 0;
+  __syncthreads();
+  if (producer && active) atomicMax(&s_nb, nb);
+  __syncthreads();
+  const uint32_t NB = s_nb;
+  const uint32_t per = kC2Per == 2 && NB >= kC2PairMinBlocks ? 2u : 1u;  // blocks per barrier
+  if (producer) {
+    uint32_t raw[16], w[16];
+    if (active) load_block16<MODE>(pa, raw);
+    for (uint32_t b = 0; b < NB; ++b) {
+      if (b < nfull) {
+        to_words(raw, w);
+      } else if (b == nfull) {
+        uint32_t rr = r;
+        asm volatile("" : "+v"(rr));
+        build_tail(raw, rr, L, w);
+      } else {
+        length_block(L, w);
+      }
+      if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
+      schedule_kw_eo(w, &kw[(b / per) & 1][b % per][lane]);
+      if (b % per == per - 1 || b + 1 == NB) __syncthreads();  // barrier g: slot g & 1 holds group g
+    }
+    __syncthreads();  // the consumers' last (they wait one group ahead)
+  } else {
+    uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
+    uint32_t H2 = eside ? 0x1f83d9abu : 0x3c6ef372u, H3 = eside ? 0x5be0cd19u : 0xa54ff53au;
+    const uint32_t sh = eside ? (sub == 1 ? 11u : sub == 2 ? 25u : 6u) : (sub == 1 ? 13u : sub == 2 ? 22u : 2u);
+    const unsigned col = (eside ? 0 : 64) + msg;  // form 4: even rounds' quads, then the odd rounds'
+#if MSHA_CHAIN2_PAIR
+    if (per == 2) {
+      uint4 ka[8], kb[8], kc[8], kd[8];
+      __syncthreads();  // barrier 0: slot 0 holds blocks 0 and 1
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        ka[q] = kw[0][0][col + q * 128];
+        kb[q] = kw[0][1][col + q * 128];
+      }
+      const uint32_t NP = (NB + 1) / 2;
+      for (uint32_t g = 0; g < NP; ++g) {
+        __syncthreads();  // barrier g + 1; reads past the last block are harmless (unused)
+        {
+          const uint32_t b = 2 * g;
+          const uint4* nk = kw[(g + 1) & 1][0];
+          MSHA_DBLOCK8(ka, kc)
+        }
+        {
+          const uint32_t b = 2 * g + 1;
+          const uint4* nk = kw[(g + 1) & 1][1];
+          MSHA_DBLOCK8(kb, kd)
+        }
+        if (++g == NP) break;
+        __syncthreads();
+        {
+          const uint32_t b = 2 * g;
+          const uint4* nk = kw[(g + 1) & 1][0];
+          MSHA_DBLOCK8(kc, ka)
+        }
+        {
+          const uint32_t b = 2 * g + 1;
+          const uint4* nk = kw[(g + 1) & 1][1];
+          MSHA_DBLOCK8(kd, kb)
+        }
+      }
+      return;
+    }
+#endif
+    uint4 ka[8], kb[8];
+    __syncthreads();  // barrier 0: slot 0 holds block 0
+#pragma unroll
+    for (int q = 0; q < 8; ++q) ka[q] = kw[0][0][col + q * 128];
+    for (uint32_t b = 0; b < NB; ++b) {
+      __syncthreads();  // barrier b + 1
+      const uint4* nk = kw[(b + 1) & 1][0];  // a read past the last block is harmless (unused)
+      MSHA_DBLOCK8(ka, kb)
+      if (++b == NB) break;
+      __syncthreads();
+      nk = kw[(b + 1) & 1][0];
+      MSHA_DBLOCK8(kb, ka)
+    }
+  }
+}
+#undef MSHA_DBLOCK8
+#undef MSHA_DQ8
+#undef MSHA_ASM8_OPERANDS
+#undef MSHA_ASM_A8
+#undef MSHA_ASM_E8
+
 #undef MSHA_DBLOCK
 #undef MSHA_DQ
 #undef MSHA_ASM_OPERANDS
@@ -1408,7 +1619,11 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
   if (n == 0) return hipSuccess;
   const uint32_t* head = gate ? gate->head : nullptr;
   if (gate && gate->head_part) {  // the planned launch's long chains, up to *head
-    if (gate->two_lane) {
+    if (gate->eight_lane) {
+      const unsigned grid = (unsigned)((n + kChain8MsgsPerWg - 1) / kChain8MsgsPerWg);
+      hipLaunchKernelGGL((k_digest_chain8<kPrefetch, true>), dim3(grid), dim3(256), 0, st, arena, off, len,
+                         order, out_idx, n, out, err, head);
+    } else if (gate->two_lane) {
       const unsigned grid = (unsigned)((n + kChain2MsgsPerWg - 1) / kChain2MsgsPerWg);
       hipLaunchKernelGGL((k_digest_chain2<kPrefetch, true>), dim3(grid), dim3(192), 0, st, arena, off, len,
                          order, out_idx, n, out, err, head);

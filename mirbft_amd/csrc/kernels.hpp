@@ -46,6 +46,7 @@ struct LaneGate {
   const uint32_t* head = nullptr;
   bool head_part = false;
   bool two_lane = false;  // head_part: k_digest_chain2 instead of the cooperative kernel
+  bool eight_lane = false;  // head_part: k_digest_chain8 (eight lanes a message, 24 a CU)
 };
 
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
@@ -59,6 +60,7 @@ bool uses_coop(uint64_t n, int cus, int policy);
 // of the two-lane head chain (k_digest_chain2).
 constexpr unsigned kCoopMsgsPerWg = 128;
 constexpr unsigned kChain2MsgsPerWg = 64;
+constexpr unsigned kChain8MsgsPerWg = 24;
 hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st, LaunchKind* kind = nullptr);
@@ -186,6 +188,7 @@ struct FoldArgs {
   uint32_t wave_block_cycles = 6500;
   uint32_t lane_cycles = 8000;
   uint32_t coop_cycles = 4200;
+  uint32_t early_cycles = 3500;  // the same for the early head's kernel (its stand-down rule)
   uint32_t head_pct = 100;
   uint32_t head_per_wg = 128;    // messages per head workgroup (one CU each)
   uint32_t tiebreak = 1;         // head-bound ties go to the cut with the most lane-kernel room (A/B: 0)

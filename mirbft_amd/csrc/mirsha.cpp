@@ -2818,9 +2818,21 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // MSHA_HEAD_CHAIN2: 0 never, 2 always (A/B).
     const uint64_t chain2_env = env_u64("MSHA_HEAD_CHAIN2", 1);
     const bool two_lane = chain2_env == 2 || (chain2_env == 1 && fold);
+    // Round 5: the EARLY head runs on the eight-lane kernel (k_digest_chain8:
+    // ~9 % fewer cycles a round, 24 messages a CU instead of 64). It exists only
+    // when its chain outlasts the lane kernel's share, so its latency is the
+    // call's; the late head (after the scan's cut, when the early head stood
+    // down: the lane kernel is the long pole) keeps the denser two-lane kernel --
+    // on it the eight-lane one took 5 CUs' worth of the lane kernel's SIMDs for
+    // c5's 100 payloads, one GPU 2.73 -> 2.84 ms (profiles/r05_chain8/).
+    // MSHA_HEAD_CHAIN8=0: the early head on the two-lane kernel too (A/B).
+    const bool eight_lane = two_lane && env_u64("MSHA_HEAD_CHAIN8", 1) != 0;
     fa.head_per_wg = two_lane ? msha::kChain2MsgsPerWg : msha::kCoopMsgsPerWg;
     fa.head_cap = head ? (uint32_t)std::min<uint64_t>(n, (uint64_t)d.cus * fa.head_per_wg) : 0;
-    fa.coop_cycles = two_lane ? 3500 : 4200;  // two-lane head: 1,427 blocks in 2.04 ms at ~2.4 GHz (r04)
+    // cycles a chain block: two-lane head 1,427 blocks in 2.04 ms at ~2.4 GHz (r04);
+    // eight-lane ~64 x 41.4 + the K+W reads and barriers (r05)
+    fa.coop_cycles = two_lane ? 3500 : 4200;
+    fa.early_cycles = eight_lane ? 3100 : 3500;
     fa.tiebreak = (uint32_t)env_u64("MSHA_PLAN_TIEBREAK", 1);
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
@@ -2836,7 +2848,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     const bool early = fold && head && two_lane && env_u64("MSHA_EARLY_HEAD", 1) != 0;
     if (early) {
       fa.long_blocks = (uint32_t)kLongBlocks;
-      fa.long_cap = (uint32_t)(d.cus * msha::kChain2MsgsPerWg / 8);
+      fa.long_cap = (uint32_t)(d.cus * (eight_lane ? msha::kChain8MsgsPerWg : msha::kChain2MsgsPerWg) / 8);
       d.f_longs.ensure(4 * (uint64_t)fa.long_cap);
       fa.longs = d.f_longs.as<uint32_t>();
       if (!d.head_stream) HIPCHK(hipStreamCreateWithFlags(&d.head_stream, hipStreamNonBlocking));
@@ -2855,6 +2867,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       eg.head = fa.info + 4;
       eg.head_part = true;
       eg.two_lane = true;
+      eg.eight_lane = eight_lane;
       msha::LaunchKind ek;
       HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, fa.longs, nullptr, fa.long_cap, d_out,
                                        d.err.as<uint32_t>(), d.cus, MSHA_KERNEL_COOP, d.head_stream, nullptr,

@@ -435,7 +435,7 @@ __global__ __launch_bounds__(1024) void k_fold_tilescan(FoldArgs a, uint64_t til
     unsigned long long ss = 0, sm = 0;
     for (int w = 0; w < 16; ++w) ss += s_sum[w], sm = max(sm, s_max[w]);
     const uint64_t t_body = ss * a.wave_block_cycles / (64ull * a.simds);
-    const uint64_t t_head = sm * a.coop_cycles;
+    const uint64_t t_head = sm * a.early_cycles;
     a.info[6] = sm >= a.long_blocks && t_body < t_head ? 1u : 0u;
   }
 }
@@ -890,7 +890,7 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
     const uint64_t tot = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t lng = __hip_atomic_load(&g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t_body = tot * a.wave_block_cycles / (64ull * a.simds);
-    const uint64_t t_head = lng * a.coop_cycles;
+    const uint64_t t_head = lng * a.early_cycles;
     a.info[4] = c <= a.long_cap && t_body < t_head ? c : 0u;
   }
 }
