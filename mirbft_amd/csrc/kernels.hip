@@ -1242,9 +1242,11 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
 // rounds' quad, the a-quad the odd rounds'): the same producer, one
 // ds_read_b128 per lane per 8 rounds. DPP sources read here are written >= 2
 // instructions earlier (tools/check_dpp_hazards.py checks the built library).
-// A consumer wave is 8 messages and each consumer owns a SIMD: 3 consumer waves
-// and the producer a workgroup, 24 messages a CU (the two-lane kernel: 64) --
-// a latency kernel for the few long payloads of a folded head.
+// A consumer wave is 8 messages and each wave owns a SIMD: two producers (even
+// and odd blocks) and two consumer waves a workgroup, 16 messages a CU (the
+// two-lane kernel: 64) -- a latency kernel for the few long payloads of a
+// folded head.
+constexpr unsigned kC8Producers = 2;
 // ---------------------------------------------------------------------------
 #define MSHA_ASM_E8(X, Y, Z, W, K)                                                               \
   "v_alignbit_b32 %[s1], %[" #X "], %[" #X "], %[sh]\n\t"                                        \
@@ -1310,12 +1312,12 @@ __global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict
   if (EXCL) __builtin_amdgcn_s_setprio(3);
   const unsigned lane = threadIdx.x & 63;
   const unsigned wave = threadIdx.x >> 6;
-  const bool producer = wave == 0;
+  const bool producer = wave < kC8Producers;
   const bool eside = (lane & 4) == 0;
   const unsigned sub = lane & 3;
-  // message of this lane inside the workgroup: the producer's lanes 0-23, each
+  // message of this lane inside the workgroup: each producer's lanes 0-15, each
   // consumer wave's 8 (8 lanes each)
-  const unsigned msg = producer ? lane : (wave - 1) * 8 + (lane >> 3);
+  const unsigned msg = producer ? lane : (wave - kC8Producers) * 8 + (lane >> 3);
   const uint64_t i = (uint64_t)blockIdx.x * kChain8MsgsPerWg + msg;
   bool active = msg < kChain8MsgsPerWg && i < n && (!limit || i < *limit);
   uint64_t m = i;  // metadata index
@@ -1347,23 +1349,29 @@ __global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict
   const uint32_t NB = s_nb;
   const uint32_t per = kC2Per == 2 && NB >= kC2PairMinBlocks ? 2u : 1u;  // blocks per barrier
   if (producer) {
+    // producer w schedules blocks w, w + 2, w + 4, ...: one producer's schedule of
+    // a block (~3,160 shader cycles) outlasted the consumers' rounds (~3,010), so
+    // one producer bounded the chain (tools/chain2_anatomy 1427 8)
+    const uint32_t pw = wave;
     uint32_t raw[16], w[16];
-    if (active) load_block16<MODE>(pa, raw);
+    if (active && pw <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)pw, raw);
     for (uint32_t b = 0; b < NB; ++b) {
-      if (b < nfull) {
-        to_words(raw, w);
-      } else if (b == nfull) {
-        uint32_t rr = r;
-        asm volatile("" : "+v"(rr));
-        build_tail(raw, rr, L, w);
-      } else {
-        length_block(L, w);
+      if (b % kC8Producers == pw) {
+        if (b < nfull) {
+          to_words(raw, w);
+        } else if (b == nfull) {
+          uint32_t rr = r;
+          asm volatile("" : "+v"(rr));
+          build_tail(raw, rr, L, w);
+        } else {
+          length_block(L, w);
+        }
+        if (active && b + kC8Producers <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + kC8Producers), raw);
+        schedule_kw_eo(w, &kw[(b / per) & 1][b % per][lane]);
       }
-      if (active && b + 1 <= nfull) load_block16<MODE>(pa + 64 * (uint64_t)(b + 1), raw);
-      schedule_kw_eo(w, &kw[(b / per) & 1][b % per][lane]);
-      if (b % per == per - 1 || b + 1 == NB) __syncthreads();  // barrier g: slot g & 1 holds group g
+      if (b % per == per - 1 || b + 1 == NB) MSHA_C2_BARRIER(b / per)  // barrier g: slot g & 1 holds group g
     }
-    __syncthreads();  // the consumers' last (they wait one group ahead)
+    MSHA_C2_BARRIER((NB + per - 1) / per)  // the consumers' last (they wait one group ahead)
   } else {
     uint32_t H0 = eside ? 0x510e527fu : 0x6a09e667u, H1 = eside ? 0x9b05688cu : 0xbb67ae85u;
     uint32_t H2 = eside ? 0x1f83d9abu : 0x3c6ef372u, H3 = eside ? 0x5be0cd19u : 0xa54ff53au;
@@ -1372,7 +1380,7 @@ __global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict
 #if MSHA_CHAIN2_PAIR
     if (per == 2) {
       uint4 ka[8], kb[8], kc[8], kd[8];
-      __syncthreads();  // barrier 0: slot 0 holds blocks 0 and 1
+      MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds blocks 0 and 1
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         ka[q] = kw[0][0][col + q * 128];
@@ -1380,7 +1388,7 @@ __global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict
       }
       const uint32_t NP = (NB + 1) / 2;
       for (uint32_t g = 0; g < NP; ++g) {
-        __syncthreads();  // barrier g + 1; reads past the last block are harmless (unused)
+        MSHA_C2_BARRIER(g + 1)  // reads past the last block are harmless (unused)
         {
           const uint32_t b = 2 * g;
           const uint4* nk = kw[(g + 1) & 1][0];
@@ -1392,7 +1400,7 @@ __global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict
           MSHA_DBLOCK8(kb, kd)
         }
         if (++g == NP) break;
-        __syncthreads();
+        MSHA_C2_BARRIER(g + 1)
         {
           const uint32_t b = 2 * g;
           const uint4* nk = kw[(g + 1) & 1][0];
@@ -1408,15 +1416,15 @@ __global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict
     }
 #endif
     uint4 ka[8], kb[8];
-    __syncthreads();  // barrier 0: slot 0 holds block 0
+    MSHA_C2_BARRIER(0)  // barrier 0: slot 0 holds block 0
 #pragma unroll
     for (int q = 0; q < 8; ++q) ka[q] = kw[0][0][col + q * 128];
     for (uint32_t b = 0; b < NB; ++b) {
-      __syncthreads();  // barrier b + 1
+      MSHA_C2_BARRIER(b + 1)
       const uint4* nk = kw[(b + 1) & 1][0];  // a read past the last block is harmless (unused)
       MSHA_DBLOCK8(ka, kb)
       if (++b == NB) break;
-      __syncthreads();
+      MSHA_C2_BARRIER(b + 1)
       nk = kw[(b + 1) & 1][0];
       MSHA_DBLOCK8(kb, ka)
     }

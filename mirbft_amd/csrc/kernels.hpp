@@ -60,7 +60,7 @@ bool uses_coop(uint64_t n, int cus, int policy);
 // of the two-lane head chain (k_digest_chain2).
 constexpr unsigned kCoopMsgsPerWg = 128;
 constexpr unsigned kChain2MsgsPerWg = 64;
-constexpr unsigned kChain8MsgsPerWg = 24;
+constexpr unsigned kChain8MsgsPerWg = 16;
 hipError_t launch_digest_uniform(const uint8_t* arena, uint64_t stride, uint64_t msg_len,
                                  uint64_t n, uint8_t* out, uint32_t* err, int cus,
                                  hipStream_t st, LaunchKind* kind = nullptr);

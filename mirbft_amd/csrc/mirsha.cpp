@@ -2830,9 +2830,9 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.head_per_wg = two_lane ? msha::kChain2MsgsPerWg : msha::kCoopMsgsPerWg;
     fa.head_cap = head ? (uint32_t)std::min<uint64_t>(n, (uint64_t)d.cus * fa.head_per_wg) : 0;
     // cycles a chain block: two-lane head 1,427 blocks in 2.04 ms at ~2.4 GHz (r04);
-    // eight-lane ~64 x 41.4 + the K+W reads and barriers (r05)
+    // eight-lane (the early head): tools/chain2_anatomy 1427 8, profiles/r05_chain8/
     fa.coop_cycles = two_lane ? 3500 : 4200;
-    fa.early_cycles = eight_lane ? 3100 : 3500;
+    fa.early_cycles = eight_lane ? 3250 : 3500;  // eight-lane: 1,427 blocks in 1.93 ms at ~2.4 GHz (r05)
     fa.tiebreak = (uint32_t)env_u64("MSHA_PLAN_TIEBREAK", 1);
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model

@@ -5,7 +5,8 @@
 // s_memtime before and after every barrier; per block: the consumers' compute
 // (barrier j+1 .. barrier j+2 arrival) and wait, the producer's compute and wait,
 // in shader-clock ticks; the clock from s_memrealtime around the whole launch.
-// One JSON line. After ~0.5 s of warm launches (clock ramp).
+// One JSON line. After ~0.5 s of warm launches (clock ramp). argv[2] == 8: the
+// eight-lane head (k_digest_chain8, round 5) instead.
 // Build: hipcc --offload-arch=gfx950 -O3 -I mirbft_amd/csrc -I include -o tools/chain2_anatomy tools/chain2_anatomy.hip
 #define MSHA_CHAIN2_STAMPS 1
 #include "kernels.hip"
@@ -43,13 +44,14 @@ int main(int argc, char** argv) {
   CHECK(hipMalloc(&out, 64));
   CHECK(hipMalloc(&err, 4));
   CHECK(hipMemset(err, 0, 4));
-  CHECK(hipMalloc(&stamps, 3 * 4096 * 8));
+  CHECK(hipMalloc(&stamps, 4 * 4096 * 8));
   CHECK(hipMemcpyToSymbol(HIP_SYMBOL(msha::g_chain2_stamps), &stamps, sizeof stamps));
   hipDeviceProp_t prop;
   CHECK(hipGetDeviceProperties(&prop, 0));
   msha::LaneGate g;
   g.head_part = true;
   g.two_lane = true;
+  g.eight_lane = argc > 2 && atoi(argv[2]) == 8;
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
@@ -63,31 +65,33 @@ int main(int argc, char** argv) {
     launch();
     CHECK(hipDeviceSynchronize());
   }
-  CHECK(hipMemset(stamps, 0, 3 * 4096 * 8));
+  CHECK(hipMemset(stamps, 0, 4 * 4096 * 8));
   CHECK(hipEventRecord(e0));
   launch();
   CHECK(hipEventRecord(e1));
   CHECK(hipEventSynchronize(e1));
   float ms = 0;
   CHECK(hipEventElapsedTime(&ms, e0, e1));
-  std::vector<uint64_t> h(3 * 4096);
+  std::vector<uint64_t> h(4 * 4096);
   CHECK(hipMemcpy(h.data(), stamps, 8 * h.size(), hipMemcpyDeviceToHost));
+  // consumer wave: 1 for the two-lane kernel, 2 for the eight-lane one (waves 0-1 produce)
+  const int cw = g.eight_lane ? 2 : 1;
   auto st = [&](int wave, uint64_t j, int after) { return (double)h[wave * 4096 + 2 * j + after]; };
   const uint64_t nb = std::min<uint64_t>(NB, 2040);
   std::vector<double> c_comp, c_wait, p_comp, p_wait;
   for (uint64_t b = 1; b + 2 < nb; ++b) {  // steady state: skip the first and last blocks
-    c_comp.push_back(st(1, b + 2, 0) - st(1, b + 1, 1));  // block b: after barrier b+1 .. barrier b+2
-    c_wait.push_back(st(1, b + 1, 1) - st(1, b + 1, 0));
+    c_comp.push_back(st(cw, b + 2, 0) - st(cw, b + 1, 1));  // block b: after barrier b+1 .. barrier b+2
+    c_wait.push_back(st(cw, b + 1, 1) - st(cw, b + 1, 0));
     p_comp.push_back(st(0, b, 0) - st(0, b - 1, 1));      // block b's slot: after barrier b-1 .. barrier b
     p_wait.push_back(st(0, b, 1) - st(0, b, 0));
   }
-  const double total_ticks = st(1, nb, 1) - st(1, 0, 0);
+  const double total_ticks = st(cw, nb, 1) - st(cw, 0, 0);
   const double ghz = total_ticks / (ms * 1e-3) / 1e9;  // approx: ticks over the launch's event time
-  printf("{\"blocks\": %llu, \"kernel_ms\": %.4f, \"us_per_block\": %.4f, \"ticks_per_block\": %.1f, "
+  printf("{\"kernel\": \"%s\", \"blocks\": %llu, \"kernel_ms\": %.4f, \"us_per_block\": %.4f, \"ticks_per_block\": %.1f, "
          "\"approx_clock_ghz\": %.3f, \"consumer_compute_ticks_median\": %.1f, \"consumer_compute_ticks_mean\": %.1f, "
          "\"consumer_wait_ticks_median\": %.1f, \"consumer_wait_ticks_mean\": %.1f, "
          "\"producer_compute_ticks_median\": %.1f, \"producer_wait_ticks_median\": %.1f}\n",
-         (unsigned long long)NB, ms, ms * 1e3 / NB, total_ticks / nb, ghz, median(c_comp), mean(c_comp),
+         g.eight_lane ? "chain8" : "chain2", (unsigned long long)NB, ms, ms * 1e3 / NB, total_ticks / nb, ghz, median(c_comp), mean(c_comp),
          median(c_wait), mean(c_wait), median(p_comp), median(p_wait));
   return 0;
 }
