@@ -2,8 +2,8 @@
 """DESIGN.md's roofline table, generated from one default bench line, the
 rocprofv3 kernel summaries of the same configs and the PMC summary:
 
-    python3 tools/design_table.py profiles/r04_final/bench_default.json \\
-        profiles/r04_final profiles/r04_pmc.json
+    python3 tools/design_table.py profiles/r05_final/bench_default.json \\
+        profiles/r05_final profiles/r05_pmc.json > profiles/r05_final/design_table.md
 
 One markdown row per config: digests/s, GB/s hashed, the mean launch from the
 line's HIP events beside rocprofv3's average for the dominant kernel, roofline
@@ -36,9 +36,10 @@ def main():
     legs = {"c2": dict(line, frac=line["roofline"]["frac"], frac_at_clock=line["roofline"]["frac_at_clock"],
                        traffic=line["roofline"]["traffic"])}
     legs.update(line.get("extra_configs", {}))
-    print("| config | kernel | digests/s | GB/s hashed | mean launch, events / rocprof avg | roofline.frac "
-          "(at the line's clock) | clock GHz | VALU busy | SIMD cycles / VALU instr | HBM ÷ algorithmic |")
-    print("|---|---|---|---|---|---|---|---|---|---|")
+    print("| config | kernel | digests/s | GB/s hashed | mean launch (default line) | rocprof command: events / "
+          "rocprof avg | roofline.frac (at the line's clock) | clock GHz | VALU busy | SIMD cycles / VALU instr | "
+          "HBM ÷ algorithmic |")
+    print("|---|---|---|---|---|---|---|---|---|---|---|")
     for cfg, leg in legs.items():
         p = pmc.get(PMC_NAME.get(cfg, ""), {})
         kern = p.get("kernel", "")
@@ -46,14 +47,17 @@ def main():
         rp = rocprof_avg_us(prof_dir, cfg, kern) if kern else None
         ev_us = leg["kernel_ms_mean"] * 1e3
         rp_s = f"{rp:,.1f}" if rp is not None else "—"
+        own = os.path.join(prof_dir, f"rocprof_{cfg}_bench_line.json")  # the rocprof command's own line
+        own_us = json.load(open(own))["kernel_ms_mean"] * 1e3 if os.path.exists(own) else None
+        own_s = f"{own_us:,.1f}" if own_us is not None else "—"
         hbm = p.get("hbm_over_algorithmic")
-        print(f"| {cfg} | `{short}` | {leg['value'] / 1e9:.3g} G | {leg['gbps_hashed']:,.0f} | "
-              f"{ev_us:,.1f} / {rp_s} µs | {leg['frac']:.3f} ({leg.get('frac_at_clock', 0):.3f}) | "
-              f"{leg.get('effective_clock_ghz', 0):.2f} | {p.get('valu_busy_pct', 0):.1f} % | "
-              f"{p.get('simd_cycles_per_valu_instr', 0):.2f} | {hbm:.2f}× |" if hbm is not None else
-              f"| {cfg} | `{short}` | {leg['value'] / 1e9:.3g} G | {leg['gbps_hashed']:,.0f} | "
-              f"{ev_us:,.1f} / {rp_s} µs | {leg['frac']:.3f} | — | — | — | — |")
 
+        def f(v, fmt, suffix=""):  # a figure the PMC summary left null (unresolved clock) prints as a dash
+            return format(v, fmt) + suffix if isinstance(v, (int, float)) else "—"
+        print(f"| {cfg} | `{short}` | {leg['value'] / 1e9:.3g} G | {leg['gbps_hashed']:,.0f} | "
+              f"{ev_us:,.1f} µs | {own_s} / {rp_s} µs | {leg['frac']:.3f} ({f(leg.get('frac_at_clock'), '.3f')}) | "
+              f"{f(leg.get('effective_clock_ghz'), '.2f')} | {f(p.get('valu_busy_pct'), '.1f', ' %')} | "
+              f"{f(p.get('simd_cycles_per_valu_instr'), '.2f')} | {f(hbm, '.2f', '×')} |")
 
 if __name__ == "__main__":
     main()
