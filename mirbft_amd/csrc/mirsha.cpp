@@ -2834,6 +2834,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.coop_cycles = two_lane ? 3500 : 4200;
     fa.early_cycles = eight_lane ? 3250 : 3500;  // eight-lane: 1,427 blocks in 1.93 ms at ~2.4 GHz (r05)
     fa.tiebreak = (uint32_t)env_u64("MSHA_PLAN_TIEBREAK", 1);
+    fa.race_test = (uint32_t)env_u64("MSHA_FOLD_LONGS_SKIP_ODD", 0);
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
     fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);

@@ -695,7 +695,9 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   __shared__ uint32_t part[1024];
   __shared__ uint64_t blk[1024];
   __shared__ uint64_t best[1024];
+  __shared__ uint32_t s_long;  // lanes of >= long_blocks blocks
   const uint32_t t = threadIdx.x;
+  if (t == 0) s_long = 0;
   constexpr uint32_t per = (kFoldBuckets + 1023) / 1024;
   const uint32_t b0 = min(t * per, kFoldBuckets), b1 = min(b0 + per, kFoldBuckets);
   uint32_t s = 0;
@@ -738,8 +740,12 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   uint64_t brun = blk[t] - bl;
   uint64_t mine = ~0ull;
   uint32_t mine_h = 0;
+  // the early head's lanes must be exactly the lanes of >= long_blocks blocks:
+  // keys up to that of a long_blocks-block message (fold_key: descending classes)
+  const uint32_t klong = a.long_blocks ? fold_key((uint64_t)(a.long_blocks - 1) * 64) + 1 : 0u;
   for (uint32_t b = b0; b < b1; ++b) {  // cut before bucket b: h = run, its longest = bucket b
     const uint32_t c = a.cnt[b];
+    if (b == klong) s_long = run;
     if (c && a.head_cap) {
       const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, key_max_blocks(a, b));
       const uint64_t key = (min(cost, kCostMax) << 20) | b;
@@ -778,8 +784,16 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     const uint32_t hfill = (h + a.head_per_wg - 1) / a.head_per_wg * a.head_per_wg;
     const uint32_t late = min(min(hfill, lanes), a.head_cap);
     // an early head (k_fold_longs) is exactly the lanes of >= long_blocks blocks:
-    // the first info[4] positions of the descending order
+    // the first info[4] positions of the descending order -- unless the alias
+    // insert, running beside k_fold_longs, claimed some long payload first: that
+    // lane is then long but not on the early head's list. Then nothing is
+    // skipped: the scan's cut (late head) and the lane kernel hash every lane,
+    // the listed ones a second time with the same digests.
+#ifndef MSHA_SCAN_NO_EARLY_CHECK
+    const uint32_t early = a.long_blocks && a.info[4] == s_long ? a.info[4] : 0u;
+#else  // round 5's committed rule, for the check's regression test (tools/r05_race.sh)
     const uint32_t early = a.long_blocks ? a.info[4] : 0u;
+#endif
     a.info[0] = lanes;
     a.info[1] = early ? early : late;
     a.info[5] = early ? 0u : late;
@@ -865,6 +879,7 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
     for (uint32_t c = threadIdx.x; c < nlist; c += blockDim.x) {
       const uint64_t i = list[c];
       const uint64_t ln = a.len[i];
+      if (a.race_test && (plan_hash(a.off[i], ln) & 1)) continue;  // left to the insert (tests)
       if (fold_claim(a, i, a.off[i], ln) == (uint32_t)i) {
         sum += dev_blocks_for(ln);
         const uint32_t k = atomicAdd(&a.info[2], 1u);

@@ -80,7 +80,7 @@ def test_c5_rank_slice_routes_long_chains(engine, world, fold):
     after = engine.stats()
     assert np.array_equal(got, exp)
     if fold or world == 8:
-        # folded: the early head (the long payloads, k_fold_tilemax's list) and the scan's
+        # folded: the early head (the long payloads, k_fold_longs' list) and the scan's
         # cut (empty then) are two launches
         assert _delta(before, after, "launches_coop") == (2 if fold and _EARLY else 1)
     assert _delta(before, after, "launches_lane") == 1
@@ -282,6 +282,66 @@ def test_early_head(engine, monkeypatch, early):
     off[alias], ln[alias] = off[longs], ln[longs]
     arena = W.random_bytes(W.SEED ^ 0x300, 0, int(off.max() + ln.max()) + 64)
     w = W.Workload("many-longs", arena, off, ln)
+    assert np.array_equal(_run(engine, w, True), _expect(w))
+
+
+def _packed(ln, seed):
+    off = np.concatenate([[0], np.cumsum((ln + np.uint64(15)) // np.uint64(16) * np.uint64(16))[:-1]]).astype(np.uint64)
+    arena = W.random_bytes(W.SEED ^ seed, 0, int(off[-1] + ln[-1]) + 64)
+    return off, arena
+
+
+@pytest.mark.parametrize("case", ["clustered", "many_in_one_tile", "huge"])
+def test_early_head_batches(engine, monkeypatch, case):
+    """Folded batches around the early head's list (k_fold_longs): long payloads
+    named only inside a few tiles of 4,096 messages each (the early head runs);
+    600 distinct long payloads in the first tile with the two-lane early head
+    (cap 2,048: it runs on 600 chains); a 16 MiB + 100 B payload named four
+    times among 50,000 requests. Every digest exact."""
+    rng = np.random.default_rng(0xE4)
+    if case == "clustered":
+        n = 200_000
+        ln = np.full(n, 512, np.uint64)
+        src = rng.choice(n, 300, replace=False)
+        ln[src] = rng.integers(260 * 64, 700 * 64, src.size).astype(np.uint64)
+        off, arena = _packed(ln, 0xE41)
+        for s in src:  # four more names of each, within 6,000 messages of it
+            near = np.clip(s + rng.integers(-6000, 6000, 4), 0, n - 1)
+            near = near[near != s]
+            off[near], ln[near] = off[s], ln[s]
+    elif case == "many_in_one_tile":
+        monkeypatch.setenv("MSHA_HEAD_CHAIN8", "0")
+        n = 50_000
+        ln = np.full(n, 512, np.uint64)
+        src = rng.choice(4096, 600, replace=False)
+        ln[src] = 257 * 64
+        off, arena = _packed(ln, 0xE42)
+        dup = rng.choice(np.arange(4096, n), 600, replace=False)
+        off[dup], ln[dup] = off[src], ln[src]
+    else:
+        n = 50_000
+        ln = np.full(n, 512, np.uint64)
+        ln[7] = (1 << 24) + 100
+        ln[9000] = 300 * 64
+        off, arena = _packed(ln, 0xE43)
+        for d in (20_000, 30_000, 40_000):
+            off[d], ln[d] = off[7], ln[7]
+        off[45_000], ln[45_000] = off[9000], ln[9000]
+    w = W.Workload(f"early-head {case}", arena, off, ln)
+    assert np.array_equal(_run(engine, w, True), _expect(w))
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_early_head_insert_claims_first(engine, monkeypatch, world):
+    """k_fold_longs lists the long payloads it claims while the alias insert runs
+    beside it; a payload the insert claims first becomes a long lane that is not
+    on the early head's list. MSHA_FOLD_LONGS_SKIP_ODD=1 forces that outcome for
+    about half the payloads (those whose table hash is odd are left to the
+    insert): k_fold_scan must then skip nothing (the late head and the lane
+    kernel hash every lane). c5 slices; every digest exact. Without the scan's
+    check the lane kernel skipped lanes nobody hashed (tools/r05_race.sh)."""
+    monkeypatch.setenv("MSHA_FOLD_LONGS_SKIP_ODD", "1")
+    w = W.c5_storm(n=(1 << 23) // world // 2, first=3 * world)
     assert np.array_equal(_run(engine, w, True), _expect(w))
 
 
