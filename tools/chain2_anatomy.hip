@@ -6,9 +6,12 @@
 // (barrier j+1 .. barrier j+2 arrival) and wait, the producer's compute and wait,
 // in shader-clock ticks; the clock from s_memrealtime around the whole launch.
 // One JSON line. After ~0.5 s of warm launches (clock ramp). argv[2] == 8: the
-// eight-lane head (k_digest_chain8, round 5) instead.
+// eight-lane head (k_digest_chain8, round 5) instead. argv[3]: messages (default 1;
+// 16 fills an eight-lane workgroup: the same payload, every lane active).
 // Build: hipcc --offload-arch=gfx950 -O3 -I mirbft_amd/csrc -I include -o tools/chain2_anatomy tools/chain2_anatomy.hip
+#ifndef MSHA_ANATOMY_NO_STAMPS  // -DMSHA_ANATOMY_NO_STAMPS: the kernel's time alone (stamp fields 0)
 #define MSHA_CHAIN2_STAMPS 1
+#endif
 #include "kernels.hip"
 
 #include <algorithm>
@@ -32,20 +35,24 @@ static double mean(const std::vector<double>& v) {
 int main(int argc, char** argv) {
   const uint64_t NB = argc > 1 ? strtoull(argv[1], nullptr, 10) : 1427;
   const uint64_t L = NB * 64 - 20;  // NB blocks (the last one holds the length)
+  const uint64_t M = argc > 3 ? strtoull(argv[3], nullptr, 10) : 1;
   uint8_t *arena, *out;
   uint64_t *off, *len, *stamps;
   uint32_t* err;
   CHECK(hipMalloc(&arena, L + 64));
   CHECK(hipMemset(arena, 0x5a, L + 64));
-  CHECK(hipMalloc(&off, 8));
-  CHECK(hipMalloc(&len, 8));
-  CHECK(hipMemset(off, 0, 8));
-  CHECK(hipMemcpy(len, &L, 8, hipMemcpyHostToDevice));
-  CHECK(hipMalloc(&out, 64));
+  CHECK(hipMalloc(&off, 8 * M));
+  CHECK(hipMalloc(&len, 8 * M));
+  CHECK(hipMemset(off, 0, 8 * M));
+  std::vector<uint64_t> lens(M, L);
+  CHECK(hipMemcpy(len, lens.data(), 8 * M, hipMemcpyHostToDevice));
+  CHECK(hipMalloc(&out, 32 * M + 32));
   CHECK(hipMalloc(&err, 4));
   CHECK(hipMemset(err, 0, 4));
   CHECK(hipMalloc(&stamps, 4 * 4096 * 8));
+#ifndef MSHA_ANATOMY_NO_STAMPS
   CHECK(hipMemcpyToSymbol(HIP_SYMBOL(msha::g_chain2_stamps), &stamps, sizeof stamps));
+#endif
   hipDeviceProp_t prop;
   CHECK(hipGetDeviceProperties(&prop, 0));
   msha::LaneGate g;
@@ -57,7 +64,7 @@ int main(int argc, char** argv) {
   CHECK(hipEventCreate(&e1));
   auto launch = [&] {
     msha::LaunchKind kind;
-    CHECK(msha::launch_digest_batch(arena, off, len, nullptr, nullptr, 1, out, err, prop.multiProcessorCount,
+    CHECK(msha::launch_digest_batch(arena, off, len, nullptr, nullptr, M, out, err, prop.multiProcessorCount,
                                     2 /* MSHA_KERNEL_COOP */, 0, nullptr, &kind, &g));
   };
   const auto t0 = std::chrono::steady_clock::now();
