@@ -515,10 +515,13 @@ def extra_c5_ranks(eng, args, dev, stream, rank: int, world: int, dist, form: st
     return out
 
 
-# The two-lane head's cost of one chain block (k_digest_chain2, SIMD-shader cycles
-# at the final round-4 code, profiles/r04_pmc.json cycles_per_chain_block): a rank's
-# longest payload on the head takes ~blocks x this / clock.
-CHAIN2_CYCLES_PER_BLOCK = 3319
+# The head's cost of one chain block, shader cycles, per planned form: a rank's
+# longest payload on its head takes ~blocks x this / clock. Folded, the early head
+# runs on the eight-lane kernel (k_digest_chain8: 1,427 blocks in 1.78 ms beside the
+# lane kernel at ~2.36 GHz, profiles/r05_fold/early_head_race/, r05_chain8/ring/);
+# unfolded, on the cooperative kernel (k_digest_coop: 2.51 ms at ~2.35 GHz,
+# profiles/r05_planned_n8/).
+HEAD_CYCLES_PER_BLOCK = {"c5_planned": 4150, "c5_folded": 2950}
 
 
 def c5_rank_summary(dist, world: int, form: str, *, n, nbytes, blocks, hashed, max_blocks, elapsed, kern_ms,
@@ -526,7 +529,7 @@ def c5_rank_summary(dist, world: int, form: str, *, n, nbytes, blocks, hashed, m
     """The N-rank c5 figures from each rank's own (every rank calls it): the job's
     digests/s over the slowest rank's time, the roofline fraction of N GPUs' peak,
     and, rank by rank, its kernel time, its longest payload and the estimated share
-    of its time that payload's serial chain takes on the two-lane head (the floor
+    of its time that payload's serial chain takes on its head (the floor
     of strong scaling: DESIGN.md (e)) -- so the driver's 8-GPU node shows which
     rank and what bounds it."""
     import torch
@@ -553,12 +556,14 @@ def c5_rank_summary(dist, world: int, form: str, *, n, nbytes, blocks, hashed, m
            "kernel_ms_per_rank": per_kern, "messages_per_rank": [int(e[3]) for e in every],
            "max_blocks_per_rank": per_max}
     if form in ("c5_planned", "c5_folded"):
-        est = [b * CHAIN2_CYCLES_PER_BLOCK / (c * 1e6) for b, c in zip(per_max, per_clock)]
+        cyc = HEAD_CYCLES_PER_BLOCK[form]
+        est = [b * cyc / (c * 1e6) for b, c in zip(per_max, per_clock)]
         out["head_chain_ms_est_per_rank"] = est
         out["head_share_est_per_rank"] = [e / k if k > 0 else None for e, k in zip(est, per_kern)]
-        out["head_chain_note"] = ("a rank's longest payload on the two-lane head: max_blocks x %d cycles "
-                                  "(k_digest_chain2, PMC) / the rank's measured clock; share = that / the rank's "
-                                  "kernel_ms (near 1: the chain bounds the rank)" % CHAIN2_CYCLES_PER_BLOCK)
+        out["head_chain_note"] = ("a rank's longest payload on its head: max_blocks x %d cycles (%s, measured in "
+                                  "situ) / the rank's measured clock; share = that / the rank's kernel_ms (near 1: "
+                                  "the chain bounds the rank)"
+                                  % (cyc, "k_digest_chain8" if form == "c5_folded" else "k_digest_coop"))
     return out
 
 

@@ -160,7 +160,7 @@ def test_eight_rank_c5_line_reports_each_rank():
             assert "head_share_est_per_rank" not in e
         else:
             est = e["head_chain_ms_est_per_rank"]
-            assert len(est) == world and abs(est[0] - 1427 * bench.CHAIN2_CYCLES_PER_BLOCK / 2.3e6) < 1e-9
+            assert len(est) == world and abs(est[0] - 1427 * bench.HEAD_CYCLES_PER_BLOCK[form] / 2.3e6) < 1e-9
             assert all(0 < s < 2 for s in e["head_share_est_per_rank"])
     # host_api: per-GPU upload GB/s from a --mode lib line over 8 GPUs
     shards = [{"device": g, "messages": 1 << 20, "lanes": 1 << 20, "head_lanes": 12, "h2d_bytes": 480e6,
