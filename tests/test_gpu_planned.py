@@ -33,7 +33,12 @@ def _expect(w, threads=16):
     return d[inv.reshape(-1)]
 
 
-_EARLY = os.environ.get("MSHA_EARLY_HEAD", "1") == "1"
+def _early(fold):
+    """Does a planned call start an early head (read when the call is made)? Folded
+    calls do, unless it is off or the head is held to the cooperative kernel
+    (MSHA_HEAD_CHAIN2=0: the early head runs on the chain kernels)."""
+    return (fold and os.environ.get("MSHA_EARLY_HEAD", "1") != "0"
+            and os.environ.get("MSHA_HEAD_CHAIN2", "1") != "0")
 
 
 def _run(engine, w, fold, stream=None):
@@ -82,7 +87,7 @@ def test_c5_rank_slice_routes_long_chains(engine, world, fold):
     if fold or world == 8:
         # folded: the early head (the long payloads, k_fold_longs' list) and the scan's
         # cut (empty then) are two launches
-        assert _delta(before, after, "launches_coop") == (2 if fold and _EARLY else 1)
+        assert _delta(before, after, "launches_coop") == (2 if _early(fold) else 1)
     assert _delta(before, after, "launches_lane") == 1
 
 
@@ -269,7 +274,7 @@ def test_early_head(engine, monkeypatch, early):
         w = W.c5_storm(n=(1 << 23) // world // 4, first=world)
         before = engine.stats()
         assert np.array_equal(_run(engine, w, True), _expect(w))
-        assert _delta(before, engine.stats(), "launches_coop") == (2 if early == "1" else 1)
+        assert _delta(before, engine.stats(), "launches_coop") == (2 if _early(True) else 1)
     # 3,000 distinct 300-block payloads (> 256 CUs x 64 / 8): no early head
     rng = np.random.default_rng(300)
     n = 60_000
@@ -367,7 +372,7 @@ def test_big_bucket_messages_head(engine, monkeypatch):
             assert np.array_equal(_run(engine, w, fold), exp)
             # the long chains got a head (folded on the two-lane kernel: the early
             # head and the scan's cut, two launches)
-            assert _delta(before, engine.stats(), "launches_coop") == (2 if fold and chain2 == "2" and _EARLY else 1)
+            assert _delta(before, engine.stats(), "launches_coop") == (2 if _early(fold) else 1)
 
 
 def test_graph_capture_refused_cleanly(engine):
