@@ -336,6 +336,23 @@ def test_early_head_batches(engine, monkeypatch, case):
     assert np.array_equal(_run(engine, w, True), _expect(w))
 
 
+def test_tile_backrefs(engine):
+    """Candidates-first folding across tiles: a message skips the alias table only
+    when its offset is above every earlier message's, which the tile prefix
+    (k_fold_tilemax, k_fold_tilescan) carries from tile to tile. Here every tile
+    of 4,096 messages names payloads of the tile before it again (10 % of its
+    messages). Every digest exact."""
+    rng = np.random.default_rng(0x1B)
+    n = 300_000
+    ln = rng.integers(0, 700, n).astype(np.uint64)
+    off, arena = _packed(ln, 0xE44)
+    back = rng.random(n) < 0.1
+    src = np.clip(np.arange(n) - 4096 - rng.integers(0, 4096, n), 0, n - 1)
+    off[back], ln[back] = off[src[back]], ln[src[back]]
+    w = W.Workload("tile-backrefs", arena, off, ln)
+    assert np.array_equal(_run(engine, w, True), _expect(w))
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_early_head_insert_claims_first(engine, monkeypatch, world):
     """k_fold_longs lists the long payloads it claims while the alias insert runs
