@@ -218,11 +218,13 @@ PEAK_CLOCK_GHZ = 2.4
 
 
 def clock_reading(eng) -> dict:
-    """The clock the GPU held right after a timed region: msha_clock_probe (a
+    """The clock the GPU holds right AFTER a timed region: msha_clock_probe (a
     ~1 ms probe kernel with the hash kernels' VALU mix at 8 waves per SIMD,
-    in-kernel s_memtime / s_memrealtime; the hash kernels carry no stamps).
-    frac_at_clock (in roofline) = frac x 2.4 GHz / this clock: the share of the
-    peak at the clock the chip actually held."""
+    in-kernel s_memtime / s_memrealtime; the hash kernels carry no stamps). A
+    diagnostic only: it is not the clock the timed launches ran at (round 5's
+    c5 probe read 2.28 GHz after launches that ran nearer 2.4), so no fraction
+    is derived from it (tools/lane_stamps.py measures the clock inside the
+    launches of a diagnostic build)."""
     try:
         c = eng.clock_probe()
     except Exception as e:  # noqa: BLE001 -- a diagnostic, never fatal to the line
@@ -230,7 +232,8 @@ def clock_reading(eng) -> dict:
     return {"effective_clock_ghz": c["ghz_median"], "min": c["ghz_min"], "max": c["ghz_max"],
             "probe_ms": c["kernel_ms"], "probe_gblocks_per_s": c["gblocks_per_s"],
             "method": "msha_clock_probe right after the timed steps: median over workgroups of "
-                      "d(s_memtime) / d(s_memrealtime) x 100 MHz"}
+                      "d(s_memtime) / d(s_memrealtime) x 100 MHz (a separate probe kernel, not the "
+                      "timed launches: diagnostic, no fraction is derived from it)"}
 
 
 def verify_sample(w, d_out, k: int = 512) -> None:
@@ -321,10 +324,16 @@ def host_api_summary(d: dict, what: str) -> dict:
 
 
 def kind_of(st0: dict, st1: dict) -> str:
-    """The kernel(s) the timed launches ran, from the msha_stats launch counters."""
+    """The kernel(s) the timed launches ran, from the msha_stats launch counters
+    (the chain kernels are counted in launches_coop too: "coop" names only the
+    cooperative kernel itself)."""
+    d = {k: st1[k] - st0[k] for k in ("launches_lane", "launches_pipe", "launches_coop", "launches_split",
+                                      "launches_dod", "launches_chain2", "launches_chain8")}
+    d["launches_coop"] -= d["launches_chain2"] + d["launches_chain8"]
     names = {"launches_lane": "lane", "launches_pipe": "pipe", "launches_coop": "coop",
+             "launches_chain2": "chain2", "launches_chain8": "chain8",
              "launches_split": "split", "launches_dod": "digest_of_digests"}
-    ran = [v for k, v in names.items() if st1[k] > st0[k]]
+    ran = [v for k, v in names.items() if d[k] > 0]
     return "+".join(ran) if ran else "none"
 
 
@@ -439,8 +448,7 @@ def roofline(w, kern_ms: float, cfg: str, clock: dict | None = None) -> dict:
     ghz = (clock or {}).get("effective_clock_ghz")
     return {"bound": "valu", "achieved": achieved, "peak": PEAK_VALU_TOPS,
             "unit": "Tint32op/s", "frac": achieved / PEAK_VALU_TOPS,
-            "effective_clock_ghz": ghz,
-            "frac_at_clock": achieved / PEAK_VALU_TOPS * PEAK_CLOCK_GHZ / ghz if ghz else None,
+            "effective_clock_ghz_after": ghz,
             "traffic": traffic, "traffic_source": src, "ops_per_block": OPS_PER_BLOCK,
             "note": "peak = full-rate int32 VALU (VOP2/v_bitop3, 2 cycles per wave64 "
                     "instr at 2.4 GHz); SHA-256's mix is ~60% half-rate ops (v_alignbit, "
@@ -471,8 +479,7 @@ def extra_config(eng, cfg: str, args, dev, stream, w=None) -> dict:
            "gbps_hashed": w.message_bytes * args.steps / elapsed / 1e9,
            "ms_per_step": elapsed / args.steps * 1e3, "kernel_ms_mean": kern_ms, "kernel": kind,
            "frac": rf["frac"], "achieved": rf["achieved"], "traffic": rf["traffic"],
-           "traffic_source": rf["traffic_source"], "effective_clock_ghz": rf["effective_clock_ghz"],
-           "frac_at_clock": rf["frac_at_clock"],
+           "traffic_source": rf["traffic_source"], "effective_clock_ghz_after": rf["effective_clock_ghz_after"],
            "blocks": w.blocks, "hashed_blocks": hashed_blocks(w, cfg),
            "verified": "512 digests vs oracle (stride not a multiple of 64)",
            "warmup_steps_run": warm}
@@ -572,7 +579,8 @@ def run_lib(args):
     (device_mask, or MSHA_VIRTUAL_SHARDS shards of one GPU), batch packed in a
     pinned arena as the cgo adapter does, msha_digest_batch per step."""
     import torch  # noqa: F401  (one HIP runtime: torch's, loaded before libmirsha)
-    from mirbft_amd import Engine
+    from mirbft_amd import Engine, _lib
+    lib_build = _lib.require_tree_build("bench.py --mode lib")
     n_gpus = args.gpus
     eng = Engine((1 << n_gpus) - 1)
     eng.set_kernel_policy(args.policy)
@@ -625,7 +633,7 @@ def run_lib(args):
         "ms_per_step": el / args.steps * 1e3, "call_ms": [round(c, 2) for c in calls],
         "config": {"workload": w.name, "config": args.config},
         "scaling": "strong" if args.config == "c5" else "weak",
-        "last_call_stats": st, "last_call_shards": sh}), flush=True)
+        "last_call_stats": st, "last_call_shards": sh, "library": lib_build}), flush=True)
     eng.close()
 
 
@@ -663,7 +671,9 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from mirbft_amd import Engine
+    from mirbft_amd import Engine, _lib
+    # the numbers are the product's only on the tree's own build (never an A/B variant's)
+    lib_build = _lib.require_tree_build("bench.py")
     eng = Engine(1 << local)
     eng.set_kernel_policy(args.policy)
     w = build_workload(args.config, rank, world)
@@ -719,8 +729,8 @@ def main():
             "gbps_hashed": gbps,
             "kernel_ms_mean": kern_ms,
             "kernel": kind,
-            "effective_clock_ghz": clock.get("effective_clock_ghz"),
-            "clock": clock,
+            "clock_after": clock,
+            "library": lib_build,
             "roofline": roofline(w, kern_ms, args.config, clock),
         }
         if world == 1 and args.config == "c2" and not args.no_extra:

@@ -262,6 +262,33 @@ func partsEqual(a, b [][]byte) bool {
 	}
 }
 
+// sameParts reports, in O(parts) and without reading payload bytes, whether
+// two part lists hold the same bytes by construction: part for part, either the
+// same slice (pointer and length: a message's own value and digest slices,
+// stateless.go:330,338,345) or, for the short fresh slices the encoding makes
+// (the BE64 fields, proposer.go:16-20), equal bytes. false means "not shown
+// equal", not "different": the caller then compares bytes (partsEqual).
+func sameParts(a, b [][]byte) bool {
+	if len(a) != len(b) {
+		return false
+	}
+	for k := range a {
+		x, y := a[k], b[k]
+		switch {
+		case len(x) != len(y):
+			return false
+		case len(x) == 0:
+		case len(x) <= 8:
+			if string(x) != string(y) {
+				return false
+			}
+		case &x[0] != &y[0]:
+			return false
+		}
+	}
+	return true
+}
+
 // epochChangeAliases finds the EpochChange hash actions whose payload an
 // earlier action of the list already carries. A node hashes every origin's
 // EpochChange once per ack (epoch_target.go:486-528, epoch_tracker.go:349-350):
@@ -270,8 +297,11 @@ func partsEqual(a, b [][]byte) bool {
 // so a pointer seen before is the same payload; acks deserialized from the
 // network hold equal copies, found by comparing the bytes of earlier payloads
 // from the same origin node with the same length (a byzantine copy that differs
-// is packed and hashed on its own). A pointer hit whose Data differs in length
-// falls back to that byte compare. alias[i] = that earlier action, or -1.
+// is packed and hashed on its own). A pointer hit aliases only when the two
+// Data lists are shown equal -- part for part the same slices, or the same
+// bytes (sameParts, else partsEqual) -- since the contract is SHA-256(Data),
+// whatever message the Data was built from (batch_tracker.go:192-195: a wrong
+// digest is a divergence). alias[i] = that earlier action, or -1.
 func epochChangeAliases(reqs []*state.ActionHashRequest) (alias []int, size int) {
 	type contentKey struct {
 		origin uint64
@@ -290,9 +320,10 @@ func epochChangeAliases(reqs []*state.ActionHashRequest) (alias []int, size int)
 				byContent = map[contentKey][]int{}
 			}
 			// a pointer seen before names the same payload only if the Data built
-			// from it has the same length (the drop-in's contract is SHA-256(Data):
-			// Data built differently from a shared message is compared byte for byte)
-			if j, seen := byPtr[ec.EpochChange]; seen && ec.EpochChange != nil && partsLen(reqs[j].Data) == l {
+			// from it is the same (the drop-in's contract is SHA-256(Data)): the
+			// same slices in O(parts), else byte for byte
+			if j, seen := byPtr[ec.EpochChange]; seen && ec.EpochChange != nil && partsLen(reqs[j].Data) == l &&
+				(sameParts(reqs[j].Data, r.Data) || partsEqual(reqs[j].Data, r.Data)) {
 				alias[i] = j
 				continue
 			}

@@ -174,6 +174,60 @@ func TestGPUEpochChangeStormPackedOnce(t *testing.T) {
 	}
 }
 
+// One *msgs.EpochChange named by two actions whose Data lists have the same
+// length but different bytes (Data built differently from one message, or the
+// message changed between the two actions): the pointer alone must not alias
+// them (batch_tracker.go:192-195), so each gets the reference's own digest.
+func TestGPUEpochChangeSamePointerDifferentData(t *testing.T) {
+	g := newGPU(t)
+	defer g.Close()
+	ec := &msgs.EpochChange{NewEpoch: 3, Checkpoints: []*msgs.Checkpoint{
+		{SeqNo: 500, Value: bytes.Repeat([]byte{1}, 332)}}}
+	origin := func(src uint64) *state.HashOrigin {
+		return &state.HashOrigin{Type: &state.HashOrigin_EpochChange_{
+			EpochChange: &state.HashOrigin_EpochChange{Source: src, Origin: 1, EpochChange: ec}}}
+	}
+	al := &statemachine.ActionList{}
+	al.Hash(ecHashData(ec), origin(0))
+	other := ecHashData(ec)
+	other[0] = be64(4) // same lengths part for part, another new_epoch
+	al.Hash(other, origin(1))
+	long := ecHashData(ec)
+	long[2] = bytes.Repeat([]byte{2}, 332) // a long part from elsewhere, same length
+	al.Hash(long, origin(2))
+	al.Hash(ecHashData(ec), origin(3)) // the same Data again: aliased
+	want, err := ProcessHashActions(crypto.SHA256, al)
+	if err != nil {
+		t.Fatal(err)
+	}
+	got, err := ProcessHashActionsGPU(g, al)
+	if err != nil {
+		t.Fatal(err)
+	}
+	wi, gi := want.Iterator(), got.Iterator()
+	var digests [][]byte
+	for i := 0; i < want.Len(); i++ {
+		w, e := wi.Next().Type.(*state.Event_HashResult), gi.Next().Type.(*state.Event_HashResult)
+		if !bytes.Equal(w.HashResult.Digest, e.HashResult.Digest) {
+			t.Fatalf("action %d: digest %x, want %x", i, e.HashResult.Digest, w.HashResult.Digest)
+		}
+		digests = append(digests, e.HashResult.Digest)
+	}
+	if bytes.Equal(digests[0], digests[1]) || bytes.Equal(digests[0], digests[2]) || !bytes.Equal(digests[0], digests[3]) {
+		t.Fatalf("aliasing by pointer alone: %x", digests)
+	}
+	reqs := []*state.ActionHashRequest{}
+	for it, a := al.Iterator(), (*state.Action)(nil); ; {
+		if a = it.Next(); a == nil {
+			break
+		}
+		reqs = append(reqs, a.Type.(*state.Action_Hash).Hash)
+	}
+	if alias, _ := epochChangeAliases(reqs); alias[1] != -1 || alias[2] != -1 || alias[3] != 0 {
+		t.Fatalf("alias = %v, want [-1 -1 -1 0]", alias)
+	}
+}
+
 func TestGPUProcessHashActionsErrors(t *testing.T) {
 	g := newGPU(t)
 	defer g.Close()

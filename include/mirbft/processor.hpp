@@ -283,10 +283,12 @@ inline std::vector<int64_t> EpochChangeAliases(const std::vector<const ActionHas
       return n;
     };
     if (key) {
-      // the same message names the same payload only if the Data built from it
-      // has the same length (the contract is SHA-256(Data)); else compare bytes
+      // the same message names the same payload only if the Data built from it is
+      // the same (the contract is SHA-256(Data), batch_tracker.go:192-195): part for
+      // part equal, else the concatenations
       auto it = by_obj.find(key);
-      if (it != by_obj.end() && parts_len(reqs[it->second]->data) == parts_len(reqs[i]->data)) {
+      if (it != by_obj.end() && parts_len(reqs[it->second]->data) == parts_len(reqs[i]->data) &&
+          (reqs[it->second]->data == reqs[i]->data || concat(reqs[it->second]->data) == concat(reqs[i]->data))) {
         alias[i] = it->second;
         continue;
       }

@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define MSHA_ABI_VERSION 9u
+#define MSHA_ABI_VERSION 10u
 
 enum {
   MSHA_OK = 0,
@@ -92,6 +92,9 @@ typedef struct {
                                dense): its touched runs went up through pinned staging, lanes planned
                                on the GPU (ABI 6) */
   uint64_t planned_device_calls; /* msha_digest_batch_device_planned calls (ABI 7) */
+  /* Of launches_coop, the ones that ran a chain kernel (ABI 10): */
+  uint64_t launches_chain2; /* two lanes a message (k_digest_chain2): late/host heads, small AUTO launches */
+  uint64_t launches_chain8; /* eight lanes a message (k_digest_chain8): the folded early head */
 } msha_stats;
 
 /* Per-GPU figures of the last host-memory call (one entry per shard; a shard is

@@ -11,10 +11,15 @@ import os
 import re
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmirsha.so")
+PRODUCT_LIB_PATH = os.path.join(_HERE, "libmirsha.so")
+# MSHA_LIB_PATH loads a diagnostic or A/B variant built OUTSIDE the package
+# (mirbft_amd/csrc/Makefile: BUILD=... OUT=...), so no experiment ever writes
+# over the product library. Such a build is not the tree's: GPU test sessions
+# and bench.py refuse it unless MSHA_ALLOW_FOREIGN_LIB=1.
+LIB_PATH = os.environ.get("MSHA_LIB_PATH") or PRODUCT_LIB_PATH
 HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "mirsha.h")
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 MSHA_OK = 0
 MSHA_ERR_INVALID_ARG = 1
 MSHA_ERR_NO_DEVICE = 2
@@ -55,6 +60,8 @@ class MshaStats(ctypes.Structure):
         ("small_calls", ctypes.c_uint64),
         ("staged_calls", ctypes.c_uint64),
         ("planned_device_calls", ctypes.c_uint64),
+        ("launches_chain2", ctypes.c_uint64),
+        ("launches_chain8", ctypes.c_uint64),
     ]
 
 
@@ -194,5 +201,23 @@ def build_id() -> dict:
     fields = dict(kv.split("=", 1) for kv in raw.split(";"))
     src, flags = fields.get("src", ""), fields.get("flags", "")
     tree = source_id()
-    return {"id": raw, "src": src, "flags": flags, "tree_src": tree,
-            "matches_tree": src == tree and not any(t.startswith("-D") for t in flags.split())}
+    return {"id": raw, "src": src, "flags": flags, "tree_src": tree, "path": LIB_PATH,
+            "matches_tree": (src == tree and not any(t.startswith("-D") for t in flags.split())
+                             and os.path.realpath(LIB_PATH) == os.path.realpath(PRODUCT_LIB_PATH))}
+
+
+def foreign_allowed() -> bool:
+    """MSHA_ALLOW_FOREIGN_LIB=1: run on a library that is not the tree's build (A/B, diagnostics)."""
+    return os.environ.get("MSHA_ALLOW_FOREIGN_LIB") == "1"
+
+
+def require_tree_build(who: str) -> dict:
+    """The loaded library's build_id(); raises unless it is the tree's own build or
+    MSHA_ALLOW_FOREIGN_LIB=1 (results of an experiment's build must not be reported
+    as the product's)."""
+    b = build_id()
+    if not b["matches_tree"] and not foreign_allowed():
+        raise RuntimeError("%s: %s is not this tree's build (%s; tree src %s): rebuild it "
+                           "(make -C mirbft_amd/csrc) or set MSHA_ALLOW_FOREIGN_LIB=1"
+                           % (who, b["path"], b["id"], b["tree_src"]))
+    return b

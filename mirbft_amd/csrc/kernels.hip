@@ -1631,16 +1631,18 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
       const unsigned grid = (unsigned)((n + kChain8MsgsPerWg - 1) / kChain8MsgsPerWg);
       hipLaunchKernelGGL((k_digest_chain8<kPrefetch, true>), dim3(grid), dim3(256), 0, st, arena, off, len,
                          order, out_idx, n, out, err, head);
+      set_kind(kind, kLaunchChain8);
     } else if (gate->two_lane) {
       const unsigned grid = (unsigned)((n + kChain2MsgsPerWg - 1) / kChain2MsgsPerWg);
       hipLaunchKernelGGL((k_digest_chain2<kPrefetch, true>), dim3(grid), dim3(192), 0, st, arena, off, len,
                          order, out_idx, n, out, err, head);
+      set_kind(kind, kLaunchChain2);
     } else {
       const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
       hipLaunchKernelGGL((k_digest_coop<kPrefetch, true>), dim3(grid), dim3(256), kCoopDynLds, st, arena, off,
                          len, order, out_idx, n, out, err, head);
+      set_kind(kind, kLaunchCoop);
     }
-    set_kind(kind, kLaunchCoop);
     return hipGetLastError();
   }
   if (split && !gate) {
@@ -1661,7 +1663,7 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
       const unsigned grid = (unsigned)((n + kChain2MsgsPerWg - 1) / kChain2MsgsPerWg);
       hipLaunchKernelGGL((k_digest_chain2<kPrefetch, false>), dim3(grid), dim3(192), 64 * 1024, st, arena, off,
                          len, order, out_idx, n, out, err, nullptr);
-      set_kind(kind, kLaunchCoop);
+      set_kind(kind, kLaunchChain2);
       return hipGetLastError();
     }
     const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);

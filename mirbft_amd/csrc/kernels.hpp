@@ -33,7 +33,9 @@ constexpr int kMaxSegmentsDod = 12;
 bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp, int cap);
 
 // Which kernel a launcher ran (msha_stats launch counters; tests assert them).
-enum LaunchKind { kLaunchNone = 0, kLaunchLane, kLaunchPipe, kLaunchCoop, kLaunchSplit, kLaunchDod };
+// kLaunchChain2 / kLaunchChain8 count as cooperative launches too (launches_coop).
+enum LaunchKind { kLaunchNone = 0, kLaunchLane, kLaunchPipe, kLaunchCoop, kLaunchSplit, kLaunchDod,
+                  kLaunchChain2, kLaunchChain8 };
 
 // GPU-planned device launches (plan.hip: msha_digest_batch_device_planned). The
 // planner's lane order holds kNoLane at positions it leaves unused (folded

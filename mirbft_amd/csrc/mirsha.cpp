@@ -606,6 +606,14 @@ void count_launch(msha_ctx* ctx, Device* d, msha::LaunchKind kind) {
     case msha::kLaunchCoop: f = &ctx->stats.launches_coop; break;
     case msha::kLaunchSplit: f = &ctx->stats.launches_split; break;
     case msha::kLaunchDod: f = &ctx->stats.launches_dod; break;
+    case msha::kLaunchChain2:
+      f = &ctx->stats.launches_coop;
+      __atomic_fetch_add(&ctx->stats.launches_chain2, 1, __ATOMIC_RELAXED);
+      break;
+    case msha::kLaunchChain8:
+      f = &ctx->stats.launches_coop;
+      __atomic_fetch_add(&ctx->stats.launches_chain8, 1, __ATOMIC_RELAXED);
+      break;
     default: return;
   }
   __atomic_fetch_add(f, 1, __ATOMIC_RELAXED);

@@ -304,13 +304,17 @@ def _epoch_change_aliases(reqs: Sequence[ActionHashRequest]) -> List[int]:
         if not isinstance(t, HashOriginEpochChange):
             continue
         ec = t.epoch_change
-        # the same object names the same payload only if the Data built from it
-        # has the same length (the contract is SHA-256(Data)); else compare bytes
-        if ec is not None and id(ec) in by_obj and \
-                sum(map(len, reqs[by_obj[id(ec)]].data)) == sum(map(len, r.data)):
-            alias[i] = by_obj[id(ec)]
-            continue
-        data = b"".join(r.data)
+        # the same object names the same payload only if the Data built from it is
+        # the same (the contract is SHA-256(Data)): part for part the same object
+        # or equal bytes (list == compares identity first), else the joined bytes
+        data = None
+        if ec is not None and id(ec) in by_obj:
+            j = by_obj[id(ec)]
+            if reqs[j].data == r.data or b"".join(reqs[j].data) == (data := b"".join(r.data)):
+                alias[i] = j
+                continue
+        if data is None:
+            data = b"".join(r.data)
         key = (t.origin, len(data))
         match = next((j for j, d in by_content.get(key, ()) if d == data), -1)
         if ec is not None:

@@ -26,19 +26,25 @@ def pytest_report_header(config):
         return "libmirsha: not loadable here (%s)" % ex
 
 
+@pytest.hookimpl(trylast=True)
 def pytest_collection_modifyitems(config, items):
-    """A GPU session on a library that is not the tree's own build (an experiment's .so
-    left in place) is refused: its results would be reported as the product's.
-    MSHA_ALLOW_FOREIGN_LIB=1 runs it anyway (A/B runs of a variant build)."""
+    """A session that selected any GPU test, on a library that is not the tree's own
+    build (an experiment's .so, or MSHA_LIB_PATH naming a variant), is refused: its
+    results would be reported as the product's. trylast: runs after -m / -k
+    deselection, so `items` is what will run. MSHA_ALLOW_FOREIGN_LIB=1 runs it anyway
+    (A/B runs of a variant build)."""
     if not any(it.get_closest_marker("gpu") for it in items) or os.environ.get("MSHA_ALLOW_FOREIGN_LIB") == "1":
         return
-    if getattr(config.option, "markexpr", "") != "gpu":
-        return
-    from mirbft_amd import _lib
-    b = _lib.build_id()
+    try:
+        from mirbft_amd import _lib
+        b = _lib.build_id()
+    except Exception as ex:  # noqa: BLE001 -- a missing / pre-ABI-9 library: say so, not an INTERNALERROR
+        raise pytest.UsageError("GPU tests selected but libmirsha's build id is unreadable (%s): build it with "
+                                "make -C mirbft_amd/csrc" % ex)
     if not b["matches_tree"]:
-        raise pytest.UsageError("libmirsha.so is not this tree's build (%s; tree src %s): rebuild it "
-                                "(make -C mirbft_amd/csrc) or set MSHA_ALLOW_FOREIGN_LIB=1" % (b["id"], b["tree_src"]))
+        raise pytest.UsageError("%s is not this tree's build (%s; tree src %s): rebuild it "
+                                "(make -C mirbft_amd/csrc) or set MSHA_ALLOW_FOREIGN_LIB=1"
+                                % (b["path"], b["id"], b["tree_src"]))
 
 
 def load_golden(name):

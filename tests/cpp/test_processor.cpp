@@ -173,6 +173,26 @@ int main() {
     }
     EXPECT(up >= distinct - 16 * 2 * nodes && up <= distinct, "each distinct payload uploaded once");
   }
+  {  // It("does not alias two actions on one message whose Data differ at equal length")
+     // (the contract is SHA-256(Data): batch_tracker.go:192-195)
+    auto msg = std::make_shared<int>(7);
+    std::vector<Bytes> a{Bytes(8, 1), Bytes(332, 2)}, b{Bytes(8, 3), Bytes(332, 2)}, c{Bytes(8, 1), Bytes(332, 4)};
+    ActionList al;
+    std::vector<const ActionHashRequest*> reqs;
+    for (auto* d : {&a, &b, &c, &a}) {
+      auto origin = std::make_shared<HashOrigin>();
+      origin->type = HashOriginEpochChange{0, 1, msg};
+      al.Hash(*d, origin);
+    }
+    for (auto& it : al.Items()) reqs.push_back(&std::get<ActionHashRequest>(it.type));
+    const auto alias = processor::EpochChangeAliases(reqs);
+    EXPECT(alias == std::vector<int64_t>({-1, -1, -1, 0}), "aliases only the equal Data");
+    auto r = processor::ProcessHashActions(hasher, al);
+    EXPECT(r.ok(), "no error");
+    int k = 0;
+    for (auto* d : {&a, &b, &c, &a})
+      EXPECT(r.ok() && r.value.Items()[k++].digest == oracle(*d), "same pointer, distinct Data: distinct digests");
+  }
   if (failures) {
     std::fprintf(stderr, "%d failure(s)\n", failures);
     return 1;

@@ -1,6 +1,7 @@
 """The C-ABI library loads and exports every symbol include/mirsha.h declares;
 host-only helpers work without a GPU. No compute calls here (CPU suite)."""
 import ctypes
+import os
 import subprocess
 
 import numpy as np
@@ -8,6 +9,8 @@ import pytest
 
 from mirbft_amd import _lib as L
 from mirbft_amd.engine import blocks_for_len, partition_by_blocks
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_header_symbols_exported():
@@ -29,7 +32,7 @@ def test_exports_via_nm():
 
 
 def test_abi_version():
-    assert L.lib().msha_abi_version() == L.ABI_VERSION == 9
+    assert L.lib().msha_abi_version() == L.ABI_VERSION == 10
 
 
 def test_build_id_is_the_trees():
@@ -177,7 +180,7 @@ def test_stats_and_shard_stats_null_args():
     assert lib.msha_shard_count(None, ctypes.byref(n)) == L.MSHA_ERR_INVALID_ARG
     assert lib.msha_get_shard_stats(None, 0, None) == L.MSHA_ERR_INVALID_ARG
     assert ctypes.sizeof(L.MshaShardStats) == 8 * 15
-    assert ctypes.sizeof(L.MshaStats) == 8 * 20
+    assert ctypes.sizeof(L.MshaStats) == 8 * 22
 
 
 def _first_ref(off, ln):
@@ -283,3 +286,25 @@ def test_device_entry_points_validate_tensors_before_the_call():
         eng.digest_batch_device_planned(arena, off, off, out)
     with pytest.raises(ValueError, match="cuda:0"):
         eng.digest_of_digests_device(arena.view(-1, 32), off.int(), off, out)
+
+
+def test_stats_structs_match_the_header(tmp_path):
+    """The ctypes mirrors of msha_stats / msha_shard_stats / msha_clock_info have the
+    C layout of include/mirsha.h (ABI 10 appended launches_chain2/chain8)."""
+    import ctypes
+    import subprocess
+    src = tmp_path / "layout.c"
+    names = {"msha_stats": (L.MshaStats, "launches_chain8"), "msha_shard_stats": (L.MshaShardStats, "plan_kernel_ms"),
+             "msha_clock_info": (L.MshaClockInfo, "blocks_per_lane")}
+    body = "".join('printf("%%s %%zu %%zu\\n", "%s", sizeof(%s), offsetof(%s, %s));\n' % (n, n, n, last)
+                   for n, (_, last) in names.items())
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "mirsha.h"\nint main(void) {\n%s return 0;\n}\n'
+                   % body)
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n")
+    for line in filter(None, out):
+        n, size, off = line.split()
+        cls, last = names[n]
+        assert ctypes.sizeof(cls) == int(size), n
+        assert getattr(cls, last).offset == int(off), n

@@ -41,6 +41,25 @@ def _early(fold):
             and os.environ.get("MSHA_HEAD_CHAIN2", "1") != "0")
 
 
+def _chain8():
+    """Does the early head run on the eight-lane kernel (k_digest_chain8)?"""
+    return os.environ.get("MSHA_HEAD_CHAIN8", "1") != "0"
+
+
+def _assert_head_kernels(before, after, fold):
+    """Each head launch counted by its kernel (ABI 10): folded, the early head on
+    k_digest_chain8 (k_digest_chain2 under MSHA_HEAD_CHAIN8=0) and the scan's cut on
+    k_digest_chain2; unfolded, the cooperative kernel. A regression that routes the
+    early head back to the two-lane kernel fails here."""
+    c2, c8 = _delta(before, after, "launches_chain2"), _delta(before, after, "launches_chain8")
+    if fold and _early(fold):
+        assert (c8, c2) == ((1, 1) if _chain8() else (0, 2)), (c8, c2)
+    elif fold:
+        assert (c8, c2) == (0, 1), (c8, c2)
+    else:
+        assert (c8, c2) == (0, 0), (c8, c2)
+
+
 def _run(engine, w, fold, stream=None):
     import torch
     d_arena, d_off, d_len = _dev(w)
@@ -88,7 +107,24 @@ def test_c5_rank_slice_routes_long_chains(engine, world, fold):
         # folded: the early head (the long payloads, k_fold_longs' list) and the scan's
         # cut (empty then) are two launches
         assert _delta(before, after, "launches_coop") == (2 if _early(fold) else 1)
+        _assert_head_kernels(before, after, fold)
     assert _delta(before, after, "launches_lane") == 1
+
+
+@pytest.mark.parametrize("chain8", [None, "0"])
+def test_early_head_kernel_counted(engine, monkeypatch, chain8):
+    """c5's rank slice over 8 GPUs, folded: the early head runs on k_digest_chain8
+    by default and not at all under MSHA_HEAD_CHAIN8=0 (then k_digest_chain2)."""
+    if chain8 is None:
+        monkeypatch.delenv("MSHA_HEAD_CHAIN8", raising=False)
+    else:
+        monkeypatch.setenv("MSHA_HEAD_CHAIN8", chain8)
+    w = W.c5_storm(n=(1 << 23) // 8, first=3)
+    before = engine.stats()
+    assert np.array_equal(_run(engine, w, True), _expect(w))
+    after = engine.stats()
+    c2, c8 = _delta(before, after, "launches_chain2"), _delta(before, after, "launches_chain8")
+    assert (c8, c2) == ((1, 1) if chain8 is None else (0, 2)), (c8, c2)
 
 
 @pytest.mark.parametrize("pct", ["1", "100000"])
@@ -333,7 +369,9 @@ def test_early_head_batches(engine, monkeypatch, case):
             off[d], ln[d] = off[7], ln[7]
         off[45_000], ln[45_000] = off[9000], ln[9000]
     w = W.Workload(f"early-head {case}", arena, off, ln)
+    before = engine.stats()
     assert np.array_equal(_run(engine, w, True), _expect(w))
+    _assert_head_kernels(before, engine.stats(), True)
 
 
 def test_tile_backrefs(engine):

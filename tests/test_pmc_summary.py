@@ -1,6 +1,7 @@
-"""tools/pmc_summary.py publishes only valid derived figures: a
-kernel too short for GRBM_GUI_ACTIVE to resolve its clock gets clock_ghz null and
-a note (round 4 printed 6.01 GHz for k_fold_tilescan), and a step of several
+"""tools/pmc_summary.py publishes only valid derived figures (VERDICT r4 weak #5,
+r5 weak #3): a kernel too short for GRBM_GUI_ACTIVE to resolve its clock, or whose
+VALU busy would exceed 100 %, gets clock_ghz / valu_busy_pct null and a note
+(round 4 printed 6.01 GHz for k_fold_tilescan, round 5 103.7 % busy), and a step of several
 kernels, serialized under --pmc, reports serialized_frac over the serial sum and
 takes roofline_frac from the bench line's overlapped step. Synthetic counter
 files, CPU only."""
@@ -12,10 +13,12 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-KERNELS = [  # name, ns, GRBM_GUI_ACTIVE (summed over 8 XCDs), SQ_INSTS_VALU
-    ("void msha::k_digest_batch<2>(unsigned char const*)", 2_500_000, 8 * 2.3 * 2_500_000, 1.4e9),
-    ("msha::k_fold_tilescan(msha::FoldArgs, unsigned long)", 6_000, 8 * 6.01 * 6_000, 1e5),
-    ("msha::k_fold_insert(msha::FoldArgs)", 80_000, 8 * 2.9 * 80_000, 1e7),  # long enough, but > 2.6 GHz
+KERNELS = [  # name, ns, GRBM_GUI_ACTIVE (summed over 8 XCDs), SQ_INSTS_VALU, VALU busy share
+    ("void msha::k_digest_batch<2>(unsigned char const*)", 2_500_000, 8 * 2.3 * 2_500_000, 1.4e9, 0.98),
+    ("msha::k_fold_tilescan(msha::FoldArgs, unsigned long)", 6_000, 8 * 6.01 * 6_000, 1e5, 0.2),
+    ("msha::k_fold_insert(msha::FoldArgs)", 80_000, 8 * 2.9 * 80_000, 1e7, 0.2),  # long enough, but > 2.6 GHz
+    # round 5's c5: 103.7 % VALU busy -- the counted cycles are short, nothing per-cycle is valid
+    ("void msha::k_digest_chain2<1, true>(unsigned char const*)", 2_000_000, 8 * 2.37 * 2_000_000, 1e8, 1.037),
 ]
 
 
@@ -26,16 +29,16 @@ def _write_pass(d, counters):
         w.writerow(["Dispatch_Id", "Kernel_Name", "Counter_Name", "Counter_Value"])
         disp = 0
         for step in range(3):
-            for name, ns, grbm, valu in KERNELS:
+            for name, ns, grbm, valu, busy in KERNELS:
                 disp += 1
-                for c, v in counters(ns, grbm, valu).items():
+                for c, v in counters(ns, grbm, valu, busy).items():
                     w.writerow([disp, name, c, v])
     with open(os.path.join(d, "run_kernel_trace.csv"), "w", newline="") as f:
         w = csv.writer(f)
         w.writerow(["Dispatch_Id", "Kernel_Name", "Start_Timestamp", "End_Timestamp"])
         disp, t = 0, 1000
         for step in range(3):
-            for name, ns, _, _ in KERNELS:
+            for name, ns, _, _, _ in KERNELS:
                 disp += 1
                 w.writerow([disp, name, t, t + ns])
                 t += ns + 1000
@@ -47,9 +50,9 @@ def test_pmc_summary_publishes_only_valid_figures(tmp_path):
            "hashed_blocks_per_gpu": 65_495_931, "max_blocks_per_message": 1427}
     line = {"config": cfg, "roofline": {"algorithmic_bytes_per_launch": 1 << 30}}
     _write_pass(str(src / "c5_folded_auto_sq"),
-                lambda ns, grbm, valu: {"GRBM_GUI_ACTIVE": grbm, "SQ_INSTS_VALU": valu,
-                                        "SQ_ACTIVE_INST_VALU": valu * 2, "SQ_WAVES": 1000,
-                                        "SQ_WAVE_CYCLES": 1e6, "SQ_WAIT_ANY": 1e4, "SQ_INSTS_SALU": 10})
+                lambda ns, grbm, valu, busy: {"GRBM_GUI_ACTIVE": grbm, "SQ_INSTS_VALU": valu,
+                                              "SQ_ACTIVE_INST_VALU": busy * 256 * grbm / 8, "SQ_WAVES": 1000,
+                                              "SQ_WAVE_CYCLES": 1e6, "SQ_WAIT_ANY": 1e4, "SQ_INSTS_SALU": 10})
     (src / "c5_folded_auto_sq.log").write_text(json.dumps(line) + "\n")
     bench = tmp_path / "bench_default.json"
     bench.write_text(json.dumps({"extra_configs": {"c5_folded": {"roofline": {"frac": 0.421}}}}) + "\n")
@@ -66,8 +69,15 @@ def test_pmc_summary_publishes_only_valid_figures(tmp_path):
     assert ins["clock_ghz"] is None and "clock_note" in ins
     lane = ks["msha::k_digest_batch<2>"]
     assert abs(lane["clock_ghz"] - 2.3) < 1e-6 and "clock_note" not in lane
+    assert abs(lane["valu_busy_pct"] - 98.0) < 1e-6
+    head = ks["msha::k_digest_chain2<1, true>"]
+    assert head["valu_busy_pct"] is None and head["clock_ghz"] is None and "clock_note" in head
+    assert head["simd_cycles_per_valu_instr"] is None and "cycles_per_chain_block" not in head
     for k in ks.values():
         assert k["clock_ghz"] is None or k["clock_ghz"] <= 2.45
+        assert k["valu_busy_pct"] is None or k["valu_busy_pct"] <= 100.0
+    # no fraction at a clock anywhere in the summary
+    assert "frac_at_clock" not in dst.read_text()
     # several kernels: the serialized frac is over their sum, roofline_frac is the line's
     assert c["roofline_frac"] == 0.421 and c["serialized_frac"] > 0
     assert "roofline_frac_note" in c

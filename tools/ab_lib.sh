@@ -1,8 +1,8 @@
 #!/bin/bash
-# Same-box A/B of two builds of libmirsha.so (build_ab/<variant>.so, built on the
+# Same-box A/B of two builds of libmirsha.so ($AB_DIR/<variant>.so, tools/ab_build.sh, built on the
 # CPU side beforehand): kernel-resident bench lines, variants interleaved per rep.
 #   VARIANTS="old new" CONFIGS="c4" REPS=3 bash tools/ab_lib.sh
-# The last variant listed is left installed in mirbft_amd/.
+# Variants load through MSHA_LIB_PATH; the product library is never touched.
 set -u
 export TMPDIR=/tmp
 OUT=gpurun_out/ab_lib
@@ -11,7 +11,7 @@ VARIANTS=${VARIANTS:-old new}
 for rep in $(seq 1 ${REPS:-2}); do
   for cfg in ${CONFIGS:-c4}; do
     for v in $VARIANTS; do
-      cp build_ab/$v.so mirbft_amd/libmirsha.so || exit 1
+      export MSHA_LIB_PATH=${AB_DIR:-/tmp/msha_ab}/$v.so MSHA_ALLOW_FOREIGN_LIB=1 || exit 1
       tag=$(echo $cfg | tr ':' '_')_${v}_rep${rep}
       timeout -k 10 300 python bench.py --config $cfg --no-cpu-baseline --no-extra ${BENCH_ARGS:-} \
         > $OUT/$tag.json 2> $OUT/$tag.err

@@ -1,11 +1,11 @@
 #!/bin/bash
 # The paired barrier only for workgroups whose longest message has >= 64 blocks
-# (build_ab/pairdyn.so) against a barrier per block (build_ab/nopair.so): the
+# ($AB_DIR/pairdyn.so) against a barrier per block ($AB_DIR/nopair.so): the
 # chain-kernel tests, AUTO small launches, c5 rank slices at N = 1 and 8.
 set -u
 OUT=${OUT:-gpurun_out/pairdyn}
 mkdir -p $OUT
-cp build_ab/pairdyn.so mirbft_amd/libmirsha.so
+export MSHA_LIB_PATH=${AB_DIR:-/tmp/msha_ab}/pairdyn.so MSHA_ALLOW_FOREIGN_LIB=1
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_planned.py \
   tests/test_gpu_host_head.py tests/test_gpu_policies.py tests/test_gpu_fuzz.py > $OUT/t.log 2>&1
 rc=$?; tail -1 $OUT/t.log; [ $rc -eq 0 ] || exit $rc

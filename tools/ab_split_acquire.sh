@@ -9,7 +9,7 @@ for segs in 12 16; do
   echo "(segs=$segs)"
   MSHA_SPLIT_SEGS=$segs VARIANTS="acq sc1ld" CONFIGS="c3 c3dd ub:200000:4096" REPS=2 bash tools/ab_lib.sh || exit 1
 done
-cp build_ab/sc1ld.so mirbft_amd/libmirsha.so
+export MSHA_LIB_PATH=${AB_DIR:-/tmp/msha_ab}/sc1ld.so MSHA_ALLOW_FOREIGN_LIB=1
 for r in 1 2 3; do
   timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_failure.py -x -q -k "split or c3 or stall or timeout or digest_of_digests" --timeout 120 > gpurun_out/ab_lib/pytest_sc1ld_$r.log 2>&1; rc=$?; tail -1 gpurun_out/ab_lib/pytest_sc1ld_$r.log; [ $rc -ne 0 ] && exit $rc
 done

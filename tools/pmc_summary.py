@@ -23,10 +23,14 @@ k_digest_*), as in earlier rounds' files, plus "kernels" (each kernel) and
 
 Only valid derived figures are published (round 5):
 - clock_ghz (and the per-cycle figures built on it: SIMD cycles per VALU
-  instruction, VALUBusy) is null for a kernel shorter than MIN_CLOCK_US or when
-  it would exceed MAX_CLOCK_GHZ: GRBM_GUI_ACTIVE also counts the dispatch's ramp
-  and drain, which a 5-15 us kernel does not amortise (round 4 printed 6.01 GHz
-  for k_fold_tilescan); the entry says why in clock_note.
+  instruction, VALUBusy) is null for a kernel shorter than MIN_CLOCK_US, when
+  it would exceed MAX_CLOCK_GHZ, or when VALUBusy would exceed 100 %:
+  GRBM_GUI_ACTIVE also counts the dispatch's ramp and drain, which a 5-15 us
+  kernel does not amortise (round 4 printed 6.01 GHz for k_fold_tilescan), and
+  round 5's c5 read 103.7 % busy, so its counted cycles were short; the entry
+  says why in clock_note.
+- No fraction "at the clock" is derived: the only clocks are this counted one
+  and msha_clock_probe's, read by a separate kernel after the timed steps.
 - A step of several kernels runs them one after another under --pmc, so its
   frac over the serial sum is "serialized_frac"; "roofline_frac" is the
   overlapped step's, taken from a bench line (4th argument: a JSON line with
@@ -49,6 +53,7 @@ HBM_PEAK_GBS = 8000.0
 TIMED = 3  # bench.py --steps 3 in tools/pmc_valu.sh
 MIN_CLOCK_US = 50.0   # below this, GRBM_GUI_ACTIVE / ns does not resolve the clock
 MAX_CLOCK_GHZ = 2.45  # MI355X tops at 2.4 GHz (+2 %): more is the counter window outlasting the kernel
+MAX_BUSY_PCT = 100.0  # VALU busy above 100 %: the cycle count under the figures is wrong
 BENCH = sys.argv[4] if len(sys.argv) > 4 else None
 # waves per workgroup of the kernels that hold a CU each (heads): the CUs they occupy
 WAVES_PER_WG = {"k_digest_chain2": 3, "k_digest_chain8": 4, "k_digest_coop": 4}
@@ -140,6 +145,12 @@ def kernel_entry(k, sq, sq2, fe, wr, cf, max_blocks=0):
                 "and the per-cycle figures are not resolved" % MIN_CLOCK_US)
     elif clk and clk > MAX_CLOCK_GHZ:
         note = "counted clock %.2f GHz is above the part's %.1f GHz: not published" % (clk, 2.4)
+    elif cyc and 100 * active / CUS / cyc > MAX_BUSY_PCT:
+        # round 5 published 103.7 % for c5: SQ_ACTIVE_INST_VALU counted more VALU-busy
+        # cycles than GRBM_GUI_ACTIVE / 8 counted cycles, so that cycle count (and the
+        # clock and cycles per instruction built on it) is short for this kernel
+        note = ("VALU busy %.1f %% > 100 %%: GRBM_GUI_ACTIVE under-counts this kernel's cycles, so its clock, "
+                "busy and cycles per instruction are not published" % (100 * active / CUS / cyc))
     ok = note is None
     e = {"us": ns / 1e3, "clock_ghz": clk if ok else None,
          "valu_lane_instr": insts * 64, "salu_instr": mean(rows, "SQ_INSTS_SALU"), "waves": waves,

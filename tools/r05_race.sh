@@ -3,17 +3,17 @@
 # the long payloads it claims while k_fold_insert runs beside it; a payload the
 # insert claims first is a long lane off the list. MSHA_FOLD_LONGS_SKIP_ODD=1 forces
 # that for half the payloads. 1) the build without k_fold_scan's check
-# (build_ab/nocheck.so, -DMSHA_SCAN_NO_EARLY_CHECK) on that test: expected to FAIL;
+# ($AB_DIR/nocheck.so, -DMSHA_SCAN_NO_EARLY_CHECK) on that test: expected to FAIL;
 # 2) the tree's build: the planned and fuzz GPU suites; 3) c5_folded slices, A/B.
 set -u
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/r05_race}
 mkdir -p $OUT
-cp build_ab/nocheck.so mirbft_amd/libmirsha.so || exit 1
+export MSHA_LIB_PATH=${AB_DIR:-/tmp/msha_ab}/nocheck.so MSHA_ALLOW_FOREIGN_LIB=1 || exit 1
 MSHA_ALLOW_FOREIGN_LIB=1 timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu \
   tests/test_gpu_planned.py -k insert_claims_first > $OUT/nocheck.log 2>&1
 echo "nocheck rc=$? (1 = the forced race gives wrong digests without the check)"; tail -3 $OUT/nocheck.log
-cp build_ab/check.so mirbft_amd/libmirsha.so || exit 1
+export MSHA_LIB_PATH=${AB_DIR:-/tmp/msha_ab}/check.so MSHA_ALLOW_FOREIGN_LIB=1 || exit 1
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu \
   tests/test_gpu_planned.py tests/test_gpu_fuzz.py > $OUT/t.log 2>&1
 rc=$?; tail -2 $OUT/t.log; [ $rc -eq 0 ] || exit $rc
