@@ -94,7 +94,9 @@ typedef struct {
   uint64_t planned_device_calls; /* msha_digest_batch_device_planned calls (ABI 7) */
   /* Of launches_coop, the ones that ran a chain kernel (ABI 10): */
   uint64_t launches_chain2; /* two lanes a message (k_digest_chain2): late/host heads, small AUTO launches */
-  uint64_t launches_chain8; /* eight lanes a message (k_digest_chain8): the folded early head */
+  uint64_t launches_chain8; /* eight lanes a message (k_digest_chain8): the folded early head, small launches */
+  uint64_t small_zc_calls;  /* of small_calls, those served zero-copy: the kernel read the packed list and wrote
+                               the digests in coherent pinned memory, no H2D or D2H (ABI 10) */
 } msha_stats;
 
 /* Per-GPU figures of the last host-memory call (one entry per shard; a shard is

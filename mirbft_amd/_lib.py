@@ -62,6 +62,7 @@ class MshaStats(ctypes.Structure):
         ("planned_device_calls", ctypes.c_uint64),
         ("launches_chain2", ctypes.c_uint64),
         ("launches_chain8", ctypes.c_uint64),
+        ("small_zc_calls", ctypes.c_uint64),
     ]
 
 

@@ -26,6 +26,75 @@
 
 namespace msha {
 
+// ---------------------------------------------------------------------------
+// Wave stamps: diagnostic build only (-DMSHA_LANE_STAMPS, tools/lane_stamps.sh;
+// VERDICT r5 item 1). Every wave of the hash kernels records, from lane 0, the
+// shader clock (s_memtime) and the 100 MHz wall clock (s_memrealtime) when it
+// starts and when its last lane is done, the SIMD / CU / SE / XCD it ran on
+// (HW_ID, XCC_ID) and which kernel it was, into a buffer of its own
+// (msha_diag_stamps): the in-kernel clock, when each workgroup started, and how
+// many SIMDs each kernel held over time, for one step of a real launch. The
+// product build compiles every hook below to nothing (tools/kernel_isa.py shows
+// the kernels' code unchanged).
+// ---------------------------------------------------------------------------
+enum StampKind : uint32_t { kStampLane = 1, kStampPipe = 2, kStampChain2 = 3, kStampChain8 = 4, kStampCoop = 5 };
+#ifdef MSHA_LANE_STAMPS
+struct WaveStampRec {
+  uint64_t t0, r0, t1, r1;  // s_memtime / s_memrealtime at the wave's start and end
+  uint32_t hw_id, xcc_id, kind, block;
+  uint32_t wave, pad0;
+  uint64_t pad1;
+};
+__device__ WaveStampRec* g_wave_stamps;
+__device__ uint32_t* g_wave_stamp_count;  // [1]: records per kind (the buffer holds 5 x that)
+struct WaveStamp {
+  uint64_t t0, r0;
+  __device__ __forceinline__ WaveStamp() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
+  __device__ __forceinline__ void close(uint32_t kind) {
+    const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if ((threadIdx.x & 63) != 0 || !g_wave_stamps) return;
+    // a fixed slot per (kind, wave): a shared counter's returning atomic at every
+    // wave's end queued the waves behind it (c2's stamped step ran 2.3x longer)
+    const uint32_t per = g_wave_stamp_count[1];
+    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (w >= per) return;
+    const uint64_t k = (uint64_t)(kind - 1) * per + w;
+    WaveStampRec r;
+    r.t0 = t0;
+    r.r0 = r0;
+    r.t1 = t1;
+    r.r1 = r1;
+    r.hw_id = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW_REG_HW_ID, 32 bits
+    r.xcc_id = __builtin_amdgcn_s_getreg(20 | (15 << 11));  // HW_REG_XCC_ID, 4 bits
+    r.kind = kind;
+    r.block = blockIdx.x;
+    r.wave = threadIdx.x >> 6;
+    r.pad0 = 0;
+    r.pad1 = 0;
+    g_wave_stamps[k] = r;
+  }
+};
+#define MSHA_WAVE_STAMP_OPEN() WaveStamp wave_stamp_;
+#define MSHA_WAVE_STAMP_CLOSE(kind) wave_stamp_.close(kind);
+}  // namespace msha
+// Diagnostic build only: points the stamps at `buf` (device memory, 5 x per
+// records of 64 B: one region per StampKind, a wave's record at its wave index)
+// and `counter` (device uint32[2]: [1] = per). The caller zeroes the buffer
+// before the launch it wants; a record with t0 == 0 was not written. NULL buf:
+// stamps off.
+extern "C" int msha_diag_wave_stamps(void* buf, void* counter) {
+  msha::WaveStampRec* b = static_cast<msha::WaveStampRec*>(buf);
+  uint32_t* c = static_cast<uint32_t*>(counter);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(msha::g_wave_stamps), &b, sizeof b) != hipSuccess) return 3;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(msha::g_wave_stamp_count), &c, sizeof c) != hipSuccess) return 3;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 3;
+}
+namespace msha {
+#else
+#define MSHA_WAVE_STAMP_OPEN()
+#define MSHA_WAVE_STAMP_CLOSE(kind)
+#endif
+
 template <int MODE = 0>
 __device__ __forceinline__ void load_block16(const uint8_t* p, uint32_t (&raw)[16]) {
   typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -248,14 +317,11 @@ __device__ __forceinline__ bool check_aligned(const uint8_t* p, uint8_t* out, ui
 }
 
 template <int MODE>
-__global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restrict__ arena,
-                                                      const uint64_t* __restrict__ off,
-                                                      const uint64_t* __restrict__ len,
-                                                      const uint32_t* __restrict__ order,
-                                                      const uint32_t* __restrict__ out_idx,
-                                                      uint64_t n, uint8_t* __restrict__ out,
-                                                      uint32_t* __restrict__ err,
-                                                      const uint32_t* __restrict__ skip_below) {
+__device__ __forceinline__ void digest_batch_lane(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
+                                                  const uint64_t* __restrict__ len, const uint32_t* __restrict__ order,
+                                                  const uint32_t* __restrict__ out_idx, uint64_t n,
+                                                  uint8_t* __restrict__ out, uint32_t* __restrict__ err,
+                                                  const uint32_t* __restrict__ skip_below) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
   if (skip_below && i < *skip_below) return;  // a long chain: the cooperative launch has it
@@ -269,6 +335,20 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
   const uint8_t* p = arena + off[m];
   if (check_aligned(p, out + 32 * o, err))
     hash_message<MODE>(p, len[m], out + 32 * o);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restrict__ arena,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint64_t* __restrict__ len,
+                                                      const uint32_t* __restrict__ order,
+                                                      const uint32_t* __restrict__ out_idx,
+                                                      uint64_t n, uint8_t* __restrict__ out,
+                                                      uint32_t* __restrict__ err,
+                                                      const uint32_t* __restrict__ skip_below) {
+  MSHA_WAVE_STAMP_OPEN()
+  digest_batch_lane<MODE>(arena, off, len, order, out_idx, n, out, err, skip_below);
+  MSHA_WAVE_STAMP_CLOSE(kStampLane)
 }
 
 // k_digest_batch with the pipelined message loop; no occupancy hint (one wave
@@ -1062,7 +1142,7 @@ __device__ uint64_t* g_chain2_stamps;
 // workgroup gets a CU of its own: EXCL false there. order, out_idx and limit
 // may be null (identity, slot = message, no device-side limit).
 template <int MODE, bool EXCL>
-__global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict__ arena,
+__device__ __forceinline__ void chain2_body(const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ off,
                                                        const uint64_t* __restrict__ len,
                                                        const uint32_t* __restrict__ order,
@@ -1218,6 +1298,20 @@ __global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict
   }
 }
 
+template <int MODE, bool EXCL>
+__global__ __launch_bounds__(192) void k_digest_chain2(const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint64_t* __restrict__ len,
+                                                       const uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ out_idx,
+                                                       uint64_t n, uint8_t* __restrict__ out,
+                                                       uint32_t* __restrict__ err,
+                                                       const uint32_t* __restrict__ limit) {
+  MSHA_WAVE_STAMP_OPEN()
+  chain2_body<MODE, EXCL>(arena, off, len, order, out_idx, n, out, err, limit);
+  MSHA_WAVE_STAMP_CLOSE(kStampChain2)
+}
+
 // ---------------------------------------------------------------------------
 // Eight lanes a message (round 5; VERDICT r4 #3: the chain that bounds c5 over 8
 // GPUs). The two-lane round spends 3 of its 11 instructions on the three
@@ -1297,7 +1391,7 @@ constexpr unsigned kC8Producers = 2;
   }
 
 template <int MODE, bool EXCL>
-__global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict__ arena,
+__device__ __forceinline__ void chain8_body(const uint8_t* __restrict__ arena,
                                                        const uint64_t* __restrict__ off,
                                                        const uint64_t* __restrict__ len,
                                                        const uint32_t* __restrict__ order,
@@ -1430,6 +1524,21 @@ __global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict
     }
   }
 }
+
+template <int MODE, bool EXCL>
+__global__ __launch_bounds__(256) void k_digest_chain8(const uint8_t* __restrict__ arena,
+                                                       const uint64_t* __restrict__ off,
+                                                       const uint64_t* __restrict__ len,
+                                                       const uint32_t* __restrict__ order,
+                                                       const uint32_t* __restrict__ out_idx,
+                                                       uint64_t n, uint8_t* __restrict__ out,
+                                                       uint32_t* __restrict__ err,
+                                                       const uint32_t* __restrict__ limit) {
+  MSHA_WAVE_STAMP_OPEN()
+  chain8_body<MODE, EXCL>(arena, off, len, order, out_idx, n, out, err, limit);
+  MSHA_WAVE_STAMP_CLOSE(kStampChain8)
+}
+
 #undef MSHA_DBLOCK8
 #undef MSHA_DQ8
 #undef MSHA_ASM8_OPERANDS
@@ -1656,6 +1765,18 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
     return hipGetLastError();
   }
   if (uses_coop(n, cus, policy) && !head) {
+    static const int small8 = env_int("MSHA_SMALL_CHAIN8", 1);
+    if (policy == 0 && n <= (uint64_t)cus * kChain8MsgsPerWg && small8) {
+      // AUTO, at most 16 messages per CU (a call of a few actions: the latency
+      // path): the eight-lane chain, one workgroup per CU (64 KiB of dynamic LDS
+      // on top of its 64 KiB keeps a second one off the CU). MSHA_SMALL_CHAIN8=0:
+      // the two-lane chain below (A/B).
+      const unsigned grid = (unsigned)((n + kChain8MsgsPerWg - 1) / kChain8MsgsPerWg);
+      hipLaunchKernelGGL((k_digest_chain8<kPrefetch, false>), dim3(grid), dim3(256), 64 * 1024, st, arena, off,
+                         len, order, out_idx, n, out, err, nullptr);
+      set_kind(kind, kLaunchChain8);
+      return hipGetLastError();
+    }
     if (policy == 0 && n <= (uint64_t)cus * kChain2MsgsPerWg && env_int("MSHA_SMALL_CHAIN2", 1)) {
       // AUTO, at most 64 messages per CU: the two-lane chain, one workgroup per CU
       // (64 KiB of dynamic LDS on top of its 33 KiB keeps a second one off the CU,

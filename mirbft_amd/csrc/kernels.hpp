@@ -194,9 +194,9 @@ struct FoldArgs {
   uint32_t head_pct = 100;
   uint32_t head_per_wg = 128;    // messages per head workgroup (one CU each)
   uint32_t tiebreak = 1;         // head-bound ties go to the cut with the most lane-kernel room (A/B: 0)
-  // tests only (MSHA_FOLD_LONGS_SKIP_ODD=1): k_fold_longs leaves every long payload
-  // whose table hash is odd to the alias insert's claim -- the outcome when the
-  // insert, running beside it, claims those first (k_fold_scan's check)
+  // test build only (-DMSHA_FOLD_RACE_TEST, MSHA_FOLD_LONGS_SKIP_ODD=1): k_fold_longs
+  // leaves every long payload whose table hash is odd unlisted, a state the product
+  // kernels cannot reach, to exercise k_fold_scan's defensive check
   uint32_t race_test = 0;
 };
 // Folding only: the tile maxima and their prefix (k_fold_tilemax, k_fold_tilescan),

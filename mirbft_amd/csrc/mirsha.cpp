@@ -95,13 +95,16 @@ struct DevBuf {
 struct PinBuf {
   void* p = nullptr;
   uint64_t cap = 0;
+  // hipHostMallocCoherent: the GPU reads and writes it over PCIe uncached (the
+  // latency path's zero-copy buffers, which kernels access in place)
+  unsigned flags = hipHostMallocPortable;
   void ensure(uint64_t bytes) {
     if (bytes <= cap) return;
     if (p) HIPCHK(hipHostFree(p));
     p = nullptr;
     cap = 0;
     uint64_t want = std::max<uint64_t>(bytes + bytes / 4, 4096);
-    HIPCHK(hipHostMalloc(&p, want, hipHostMallocPortable));
+    HIPCHK(hipHostMalloc(&p, want, flags));
     cap = want;
   }
   void release() {
@@ -229,6 +232,10 @@ struct Device {
   // small-call path (run_small): [meta | payload] in, [error word | digests] out
   DevBuf sm_in, sm_out;
   PinBuf sm_stage, sm_res;
+  // zero-copy latency path: [meta | payload] and the digests in coherent pinned
+  // memory the kernel reads and writes in place (no H2D, no D2H)
+  PinBuf sm_zc_in{nullptr, 0, hipHostMallocPortable | hipHostMallocCoherent};
+  PinBuf sm_zc_out{nullptr, 0, hipHostMallocPortable | hipHostMallocCoherent};
   // direct path, planned on the GPU (plan.hip): raw metadata, granule map,
   // device offsets, alias table and slots, representatives, bucket counters,
   // [gmin | cut | info] read back to h_small; rep read back to h_rep
@@ -273,7 +280,7 @@ struct Device {
       b->release();
     if (split_flags) (void)hipFree(split_flags);
     split_flags = nullptr;
-    for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1], &sm_stage, &sm_res, &h_gmap, &h_small, &h_rep,
+    for (PinBuf* b : {&h_arena, &h_meta, &h_out, &slot[0], &slot[1], &sm_stage, &sm_res, &sm_zc_in, &sm_zc_out, &h_gmap, &h_small, &h_rep,
                       &h_head})
       b->release();
     for (hipEvent_t* e : {&ev0, &ev1, &ev_up0, &ev_up1, &ev_k0, &ev_meta, &ev_plan, &ev_p0, &ev_p1, &slot_free[0],
@@ -1034,6 +1041,71 @@ inline bool small_call(uint64_t n, uint64_t bytes) {
   return n <= small_msgs() && bytes <= small_bytes() && small_bytes() > 0;
 }
 
+// Stats of a latency-path call (run_small, run_small_zc).
+void small_stats(msha_ctx* ctx, Device& d, double t0, double t_pack, double t_dev, uint64_t m, uint64_t pay,
+                 uint64_t h2d, uint64_t d2h, bool packed, msha::LaunchKind kind) {
+  for (Device& o : ctx->devs) {
+    o.st = msha_shard_stats{};
+    o.st.device = o.id;
+  }
+  d.st.messages = d.st.lanes = m;
+  d.st.h2d_payload_bytes = pay;
+  d.st.h2d_bytes = h2d;
+  d.st.d2h_bytes = d2h;
+  d.st.device_ms = t_dev - t_pack;
+  count_launch(ctx, &d, kind);
+  ctx->stats.calls++;
+  ctx->stats.small_calls++;
+  ctx->stats.plan_ms = t_pack - t0;
+  ctx->stats.pack_ms = packed ? t_pack - t0 : 0;
+  ctx->stats.device_ms = t_dev - t_pack;
+  ctx->stats.h2d_bytes = h2d;
+  ctx->stats.d2h_bytes = d2h;
+  ctx->stats.total_ms = now_ms() - t0;
+  trace("done", t0);
+}
+
+// The zero-copy latency path (see run_small): [off | len | payload] packed into
+// coherent pinned memory, read in place by the kernel, digests written in place.
+template <class Fill>
+void run_small_zc(msha_ctx* ctx, Device& d, double t0, uint64_t m, uint64_t meta, uint64_t pay, const uint64_t* len,
+                  uint8_t* out, Fill& fill, const uint64_t* first) {
+  d.sm_zc_in.ensure(meta + pay + msha::kArenaSlack);
+  d.sm_zc_out.ensure(32 * m);
+  uint64_t* h_off = d.sm_zc_in.as<uint64_t>();
+  uint64_t* h_len = h_off + m;
+  uint8_t* h_pay = d.sm_zc_in.as<uint8_t>() + meta;
+  uint64_t a = 0;
+  for (uint64_t i = 0; i < m; ++i) {
+    h_len[i] = len[i];
+    if (first && first[i] != i) {
+      h_off[i] = h_off[first[i]];
+    } else {
+      h_off[i] = a;
+      if (len[i]) fill(i, h_pay + a);
+      a += round16(len[i]);
+    }
+  }
+  const double t_pack = now_ms();
+  HIPCHK(hipSetDevice(d.id));
+  const uint64_t out_cap = d.sm_out.cap;
+  d.sm_out.ensure(32);  // the device error word (never set here: the packer's offsets are aligned)
+  if (d.sm_out.cap != out_cap) HIPCHK(hipMemsetAsync(d.sm_out.p, 0, 32, d.stream));
+  void *dev_in = nullptr, *dev_out = nullptr;
+  HIPCHK(hipHostGetDevicePointer(&dev_in, d.sm_zc_in.p, 0));
+  HIPCHK(hipHostGetDevicePointer(&dev_out, d.sm_zc_out.p, 0));
+  const uint64_t* d_off = static_cast<const uint64_t*>(dev_in);
+  msha::LaunchKind kind;
+  HIPCHK(msha::launch_digest_batch(static_cast<const uint8_t*>(dev_in) + meta, d_off, d_off + m, nullptr, nullptr, m,
+                                   static_cast<uint8_t*>(dev_out), d.sm_out.as<uint32_t>(), d.cus, MSHA_KERNEL_AUTO,
+                                   d.stream, nullptr, &kind));
+  HIPCHK(hipStreamSynchronize(d.stream));
+  const double t_dev = now_ms();
+  std::memcpy(out, d.sm_zc_out.p, 32 * m);
+  ctx->stats.small_zc_calls++;
+  small_stats(ctx, d, t0, t_pack, t_dev, m, pay, 0, 0, true, kind);
+}
+
 // The caller's pinned arena, uploaded as is: messages i at base + off[i], all
 // inside [lo, hi), 16-byte aligned.
 struct SmallSpan {
@@ -1046,6 +1118,18 @@ struct SmallSpan {
 // len) (alias_uids): an aliased payload is packed once and its aliases point at
 // it (EpochChange re-hashes, epoch_target.go:486-505; the Go adapter shares a
 // payload between actions, gpuhash.go epochChangeAliases).
+//
+// Zero-copy (round 6): a call of at most small_zc_msgs()
+// messages and small_zc_bytes() packed (a few actions: MirBFT's hash worker at low
+// load) skips both copies. The list is packed into coherent pinned memory that the
+// kernel (the eight-lane chain: at most 16 messages a CU) reads in place over PCIe,
+// and the digests are written straight into coherent pinned memory: one launch and
+// one synchronize per call. The packer's own 16-byte aligned offsets cannot raise
+// the device error word (check_aligned), so it stays on the device.
+uint64_t small_zc_bytes() { return env_u64("MSHA_SMALL_ZC_BYTES", 64ull << 10); }  // 0 disables
+uint64_t small_zc_msgs(const Device& d) { return std::min<uint64_t>(env_u64("MSHA_SMALL_ZC_MSGS", 256),
+                                                                    (uint64_t)d.cus * msha::kChain8MsgsPerWg); }
+
 template <class Fill>
 void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_t* out, Fill&& fill,
                const SmallSpan* span = nullptr, const uint64_t* first = nullptr) {
@@ -1058,6 +1142,9 @@ void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_
     for (uint64_t i = 0; i < m; ++i)
       if (!first || first[i] == i) pay += round16(len[i]);
   }
+  const bool zc = !span && ctx->kernel_policy == MSHA_KERNEL_AUTO && m <= small_zc_msgs(d) &&
+                  meta + pay <= small_zc_bytes();
+  if (zc) return run_small_zc(ctx, d, t0, m, meta, pay, len, out, fill, first);
   d.sm_stage.ensure(meta + (span ? 0 : pay));
   uint64_t* h_off = d.sm_stage.as<uint64_t>();
   uint64_t* h_len = h_off + m;
@@ -1107,26 +1194,8 @@ void run_small(msha_ctx* ctx, double t0, uint64_t m, const uint64_t* len, uint8_
     throw MshaError(MSHA_ERR_HIP, "internal: device error flag " + std::to_string(errflag) + " on a small call");
   }
   std::memcpy(out, d.sm_res.as<uint8_t>() + 32, 32 * m);
-  for (Device& o : ctx->devs) {
-    o.st = msha_shard_stats{};
-    o.st.device = o.id;
-  }
   const uint64_t h2d = 16 * m + (span ? pay : meta - 16 * m + pay);
-  d.st.messages = d.st.lanes = m;
-  d.st.h2d_payload_bytes = pay;
-  d.st.h2d_bytes = h2d;
-  d.st.d2h_bytes = 32 + 32 * m;
-  d.st.device_ms = t_dev - t_pack;
-  count_launch(ctx, &d, kind);
-  ctx->stats.calls++;
-  ctx->stats.small_calls++;
-  ctx->stats.plan_ms = t_pack - t0;
-  ctx->stats.pack_ms = span ? 0 : t_pack - t0;
-  ctx->stats.device_ms = t_dev - t_pack;
-  ctx->stats.h2d_bytes = h2d;
-  ctx->stats.d2h_bytes = 32 + 32 * m;
-  ctx->stats.total_ms = now_ms() - t0;
-  trace("done", t0);
+  small_stats(ctx, d, t0, t_pack, t_dev, m, pay, h2d, 32 + 32 * m, !span, kind);
 }
 
 // Launch shard d's lanes accumulated since its last launch, up to the end of

@@ -784,9 +784,11 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     const uint32_t hfill = (h + a.head_per_wg - 1) / a.head_per_wg * a.head_per_wg;
     const uint32_t late = min(min(hfill, lanes), a.head_cap);
     // an early head (k_fold_longs) is exactly the lanes of >= long_blocks blocks:
-    // the first info[4] positions of the descending order -- unless the alias
-    // insert, running beside k_fold_longs, claimed some long payload first: that
-    // lane is then long but not on the early head's list. Then nothing is
+    // the first info[4] positions of the descending order. A defensive invariant,
+    // not a race the kernels can produce: whichever of k_fold_longs and the alias
+    // insert claims a long payload first, k_fold_longs claims every long message
+    // and so reads back -- and lists -- each claimant. Should the two
+    // counts ever differ (forced only by the MSHA_FOLD_RACE_TEST build), nothing is
     // skipped: the scan's cut (late head) and the lane kernel hash every lane,
     // the listed ones a second time with the same digests.
 #ifndef MSHA_SCAN_NO_EARLY_CHECK
@@ -879,7 +881,9 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
     for (uint32_t c = threadIdx.x; c < nlist; c += blockDim.x) {
       const uint64_t i = list[c];
       const uint64_t ln = a.len[i];
-      if (a.race_test && (plan_hash(a.off[i], ln) & 1)) continue;  // left to the insert (tests)
+#ifdef MSHA_FOLD_RACE_TEST  // test build only (tests/test_gpu_planned.py, tools/r06_race.sh)
+      if (a.race_test && (plan_hash(a.off[i], ln) & 1)) continue;  // left to the insert
+#endif
       if (fold_claim(a, i, a.off[i], ln) == (uint32_t)i) {
         sum += dev_blocks_for(ln);
         const uint32_t k = atomicAdd(&a.info[2], 1u);

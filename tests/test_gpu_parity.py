@@ -29,20 +29,30 @@ def _arena_from(msgs, align=16):
     return arena, np.array(offs, dtype=np.uint64), np.array([len(m) for m in msgs], dtype=np.uint64)
 
 
-@pytest.fixture(params=["small", "pipeline"])
+@pytest.fixture(params=["small", "small_copy", "pipeline"])
 def host_path(request, engine, monkeypatch):
-    """Run a host-API test through the small-call path (one H2D, one launch, one
-    D2H) and through the pipelined path (forced by MSHA_SMALL_BYTES=0), and check
-    which one ran (msha_stats.small_calls)."""
+    """Run a host-API test through the small-call path (calls of a few actions
+    zero-copy: the kernel reads the packed list and writes the digests in coherent
+    pinned memory; larger ones one H2D, one launch, one D2H), through the small path
+    with zero-copy off (MSHA_SMALL_ZC_BYTES=0) and through the pipelined path
+    (forced by MSHA_SMALL_BYTES=0), and check which one ran (msha_stats.small_calls,
+    small_zc_calls)."""
+    monkeypatch.delenv("MSHA_SMALL_ZC_BYTES", raising=False)
     if request.param == "pipeline":
         monkeypatch.setenv("MSHA_SMALL_BYTES", "0")
     else:
         monkeypatch.delenv("MSHA_SMALL_BYTES", raising=False)
         monkeypatch.delenv("MSHA_SMALL_MSGS", raising=False)
-    before = engine.stats()["small_calls"]
+        if request.param == "small_copy":
+            monkeypatch.setenv("MSHA_SMALL_ZC_BYTES", "0")
+    before = engine.stats()
     yield request.param
-    ran = engine.stats()["small_calls"] - before
-    assert ran > 0 if request.param == "small" else ran == 0
+    after = engine.stats()
+    ran = after["small_calls"] - before["small_calls"]
+    zc = after["small_zc_calls"] - before["small_zc_calls"]
+    assert ran > 0 if request.param != "pipeline" else ran == 0
+    if request.param != "small":
+        assert zc == 0
 
 
 # ---------------------------------------------------------------- fixtures --
@@ -1121,6 +1131,58 @@ def test_small_path_digest_of_digests_and_actions(engine):
     actions = [[table[k].tobytes() for k in idx[begin[i]:begin[i + 1]]] for i in range(len(counts))]
     assert engine.hash_actions(actions) == [bytes(g) for g in got]
     assert engine.stats()["small_calls"] == st0["small_calls"] + 2
+
+
+@pytest.mark.parametrize("zc", ["default", "0"])
+def test_small_path_zero_copy(engine, actions_golden, monkeypatch, zc):
+    """Calls of a few actions (MirBFT's hash worker at low load, mirbft.go:282-302)
+    run zero-copy: one launch of the eight-lane chain reading the packed list in
+    coherent pinned memory over PCIe and writing the digests there (no H2D, no
+    D2H). Every golden action alone and in small groups, request digests of one to
+    100 (under both limits' defaults), an aliased payload, empty messages; the same calls
+    with zero-copy off (MSHA_SMALL_ZC_BYTES=0) take the copying small path. Each
+    call's digests exact, each call counted by its path and kernel."""
+    if zc == "0":
+        monkeypatch.setenv("MSHA_SMALL_ZC_BYTES", "0")
+    else:
+        monkeypatch.delenv("MSHA_SMALL_ZC_BYTES", raising=False)
+    monkeypatch.delenv("MSHA_SMALL_BYTES", raising=False)
+    calls = [[parts] for _, _, parts, _ in actions_golden]
+    exp_calls = [[d] for _, _, _, d in actions_golden]
+    calls.append([parts for _, _, parts, _ in actions_golden[:7]])
+    exp_calls.append([d for _, _, _, d in actions_golden[:7]])
+    w = W.c2_requests(100)
+    reqs = [w.arena[int(o):int(o) + int(n)].tobytes() for o, n in zip(w.off, w.len)]
+    for k in (1, 2, 16, 17, 64, 100):
+        calls.append([[r] for r in reqs[:k]])
+        exp_calls.append([hashlib.sha256(r).digest() for r in reqs[:k]])
+    calls.append([[reqs[0]], [b""], [reqs[0]], [], [reqs[1][:55]], [reqs[0]]])
+    exp_calls.append([hashlib.sha256(b"".join(p)).digest() for p in calls[-1]])
+    for c, e in zip(calls, exp_calls):
+        st0 = engine.stats()
+        assert engine.hash_actions(c) == e
+        st1 = engine.stats()
+        assert st1["small_calls"] == st0["small_calls"] + 1
+        want_zc = int(zc != "0")
+        assert st1["small_zc_calls"] - st0["small_zc_calls"] == want_zc, len(c)
+        if want_zc:  # the eight-lane chain, nothing copied
+            assert st1["launches_chain8"] == st0["launches_chain8"] + 1
+            assert st1["h2d_bytes"] == 0 and st1["d2h_bytes"] == 0
+    # at and over the limits (MSHA_SMALL_ZC_MSGS; MSHA_SMALL_ZC_BYTES over the packed
+    # [off | len | payload], metadata rounded to 64 B): zero-copy, then the copying path
+    if zc == "0":
+        return
+    packed16 = (16 * 16 + 63) // 64 * 64 + 16 * 512
+    for env, val, k, fits in (("MSHA_SMALL_ZC_MSGS", "16", 16, True), ("MSHA_SMALL_ZC_MSGS", "16", 17, False),
+                              ("MSHA_SMALL_ZC_BYTES", str(packed16), 16, True),
+                              ("MSHA_SMALL_ZC_BYTES", str(packed16 - 1), 16, False)):
+        monkeypatch.setenv(env, val)
+        st0 = engine.stats()
+        got = engine.digest_batch(w.arena, w.off[:k], w.len[:k])
+        assert np.array_equal(got, oracle.digest_batch(w.arena, w.off[:k], w.len[:k]))
+        ran = engine.stats()["small_zc_calls"] - st0["small_zc_calls"]
+        assert ran == int(fits), (env, val, k)
+        monkeypatch.delenv(env)
 
 
 def test_small_path_limits(engine, monkeypatch):
