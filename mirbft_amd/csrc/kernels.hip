@@ -42,7 +42,7 @@ enum StampKind : uint32_t { kStampLane = 1, kStampPipe = 2, kStampChain2 = 3, kS
 struct WaveStampRec {
   uint64_t t0, r0, t1, r1;  // s_memtime / s_memrealtime at the wave's start and end
   uint32_t hw_id, xcc_id, kind, block;
-  uint32_t wave, pad0;
+  uint32_t wave, work;      // work: the lane kernel's largest block count in the wave | active lanes << 16
   uint64_t pad1;
 };
 __device__ WaveStampRec* g_wave_stamps;
@@ -50,8 +50,11 @@ __device__ uint32_t* g_wave_stamp_count;  // [1]: records per kind (the buffer h
 struct WaveStamp {
   uint64_t t0, r0;
   __device__ __forceinline__ WaveStamp() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
-  __device__ __forceinline__ void close(uint32_t kind) {
+  __device__ __forceinline__ void close(uint32_t kind, uint32_t nb = 0) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    uint32_t mx = nb;
+    for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
+    const uint32_t lanes = (uint32_t)__popcll(__ballot(nb != 0));
     if ((threadIdx.x & 63) != 0 || !g_wave_stamps) return;
     // a fixed slot per (kind, wave): a shared counter's returning atomic at every
     // wave's end queued the waves behind it (c2's stamped step ran 2.3x longer)
@@ -69,13 +72,14 @@ struct WaveStamp {
     r.kind = kind;
     r.block = blockIdx.x;
     r.wave = threadIdx.x >> 6;
-    r.pad0 = 0;
+    r.work = min(mx, 0xFFFFu) | (lanes << 16);
     r.pad1 = 0;
     g_wave_stamps[k] = r;
   }
 };
 #define MSHA_WAVE_STAMP_OPEN() WaveStamp wave_stamp_;
 #define MSHA_WAVE_STAMP_CLOSE(kind) wave_stamp_.close(kind);
+#define MSHA_WAVE_STAMP_CLOSE_NB(kind, nb) wave_stamp_.close(kind, nb);
 }  // namespace msha
 // Diagnostic build only: points the stamps at `buf` (device memory, 5 x per
 // records of 64 B: one region per StampKind, a wave's record at its wave index)
@@ -93,6 +97,7 @@ namespace msha {
 #else
 #define MSHA_WAVE_STAMP_OPEN()
 #define MSHA_WAVE_STAMP_CLOSE(kind)
+#define MSHA_WAVE_STAMP_CLOSE_NB(kind, nb)
 #endif
 
 template <int MODE = 0>
@@ -316,25 +321,30 @@ __device__ __forceinline__ bool check_aligned(const uint8_t* p, uint8_t* out, ui
   return false;
 }
 
+// Returns the message's length (diagnostic stamps only; 0 for an idle lane).
 template <int MODE>
-__device__ __forceinline__ void digest_batch_lane(const uint8_t* __restrict__ arena, const uint64_t* __restrict__ off,
-                                                  const uint64_t* __restrict__ len, const uint32_t* __restrict__ order,
-                                                  const uint32_t* __restrict__ out_idx, uint64_t n,
-                                                  uint8_t* __restrict__ out, uint32_t* __restrict__ err,
-                                                  const uint32_t* __restrict__ skip_below) {
+__device__ __forceinline__ uint64_t digest_batch_lane(const uint8_t* __restrict__ arena,
+                                                      const uint64_t* __restrict__ off,
+                                                      const uint64_t* __restrict__ len,
+                                                      const uint32_t* __restrict__ order,
+                                                      const uint32_t* __restrict__ out_idx, uint64_t n,
+                                                      uint8_t* __restrict__ out, uint32_t* __restrict__ err,
+                                                      const uint32_t* __restrict__ skip_below) {
   const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  if (skip_below && i < *skip_below) return;  // a long chain: the cooperative launch has it
+  if (i >= n) return 0;
+  if (skip_below && i < *skip_below) return 0;  // a long chain: the cooperative launch has it
   uint64_t m = i;                             // metadata index
   if (order) {
     const uint32_t v = order[i];
-    if (v == kNoLane) return;                 // planned launch: a folded alias's position
+    if (v == kNoLane) return 0;               // planned launch: a folded alias's position
     m = v;
   }
   const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;  // digest slot
   const uint8_t* p = arena + off[m];
+  const uint64_t l = len[m];
   if (check_aligned(p, out + 32 * o, err))
-    hash_message<MODE>(p, len[m], out + 32 * o);
+    hash_message<MODE>(p, l, out + 32 * o);
+  return l + 1;
 }
 
 template <int MODE>
@@ -347,8 +357,9 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
                                                       uint32_t* __restrict__ err,
                                                       const uint32_t* __restrict__ skip_below) {
   MSHA_WAVE_STAMP_OPEN()
-  digest_batch_lane<MODE>(arena, off, len, order, out_idx, n, out, err, skip_below);
-  MSHA_WAVE_STAMP_CLOSE(kStampLane)
+  const uint64_t l1 = digest_batch_lane<MODE>(arena, off, len, order, out_idx, n, out, err, skip_below);
+  MSHA_WAVE_STAMP_CLOSE_NB(kStampLane, l1 ? (uint32_t)((l1 - 1) >> 6) + ((((l1 - 1) & 63) < 56) ? 1u : 2u) : 0u)
+  (void)l1;
 }
 
 // k_digest_batch with the pipelined message loop; no occupancy hint (one wave

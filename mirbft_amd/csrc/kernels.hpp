@@ -157,9 +157,11 @@ struct FoldArgs {
   uint32_t* info;             // [0] lanes, [1] positions the lane kernel skips (the head's),
                               // [2] distinct long payloads, [3] k_fold_longs workgroups done,
                               // [4] the early head's lanes (0: none), [5] the late head's,
-                              // [6] k_fold_tilescan's first decision (0: no early head),
+                              // [6] the first decision (0: no early head), by k_fold_tilescan,
+                              // or with early_fork by k_fold_longs_gate ([7]: its workgroups
+                              // done, [12..15] two u64: the short blocks and longest chain),
                               // [8..11] two u64: the batch's blocks and longest chain
-                              // ([2], [3], [8..11] zeroed by the caller: 12 words)
+                              // (all 16 words zeroed by the caller)
   // The early head (folding only; long_blocks 0: off): k_fold_tilescan sizes the
   // batch (info[6]: 0 when the short messages alone outlast the longest chain);
   // unless it stood down there, k_fold_longs claims every message of >=
@@ -174,6 +176,11 @@ struct FoldArgs {
   // 16-byte vectors (plan.hip load_run)
   uint32_t vec = 0;
   uint32_t long_blocks = 0;
+  // Round 6: the early head's first decision and list run on the
+  // head's stream forked BEFORE the tile prefix (k_fold_longs_gate, a pass over len
+  // alone, then k_fold_longs), so the head's chain does not wait for the prefix;
+  // k_fold_tilemax / k_fold_tilescan then size only the offsets.
+  uint32_t early_fork = 0;
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;

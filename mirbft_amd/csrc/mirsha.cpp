@@ -12,6 +12,7 @@
 #include <unistd.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <chrono>
 #include <cstdio>
@@ -1095,11 +1096,38 @@ void run_small_zc(msha_ctx* ctx, Device& d, double t0, uint64_t m, uint64_t meta
   HIPCHK(hipHostGetDevicePointer(&dev_in, d.sm_zc_in.p, 0));
   HIPCHK(hipHostGetDevicePointer(&dev_out, d.sm_zc_out.p, 0));
   const uint64_t* d_off = static_cast<const uint64_t*>(dev_in);
+  // Completion by polling the digests themselves (MSHA_SMALL_ZC_POLL=0: a stream
+  // synchronize, A/B): every 8-byte word starts as a sentinel, and the kernel
+  // overwrites each with its final value in one PCIe write (16-byte digest halves).
+  // A word that still reads as the sentinel is waited for until hipStreamQuery
+  // reports the launch done -- so a digest word that happens to equal the
+  // sentinel (2^-64 a word) only costs the wait, never a wrong digest -- and a
+  // failed launch is reported from there.
+  const bool poll = env_u64("MSHA_SMALL_ZC_POLL", 1) != 0;
+  constexpr uint64_t kSentinel = 0xC3A55A3C96E1F00Full;
+  volatile uint64_t* words = static_cast<volatile uint64_t*>(d.sm_zc_out.p);
+  if (poll)
+    for (uint64_t k = 0; k < 4 * m; ++k) words[k] = kSentinel;
   msha::LaunchKind kind;
   HIPCHK(msha::launch_digest_batch(static_cast<const uint8_t*>(dev_in) + meta, d_off, d_off + m, nullptr, nullptr, m,
                                    static_cast<uint8_t*>(dev_out), d.sm_out.as<uint32_t>(), d.cus, MSHA_KERNEL_AUTO,
                                    d.stream, nullptr, &kind));
-  HIPCHK(hipStreamSynchronize(d.stream));
+  if (poll) {
+    uint64_t k = 0;
+    for (uint64_t spin = 1; k < 4 * m; ++spin) {
+      while (k < 4 * m && words[k] != kSentinel) ++k;
+      if (k == 4 * m || spin % 64) {
+        __builtin_ia32_pause();
+        continue;
+      }
+      const hipError_t q = hipStreamQuery(d.stream);
+      if (q == hipSuccess) break;  // done: every word is final, whatever it reads
+      if (q != hipErrorNotReady) HIPCHK(q);
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+  } else {
+    HIPCHK(hipStreamSynchronize(d.stream));
+  }
   const double t_dev = now_ms();
   std::memcpy(out, d.sm_zc_out.p, 32 * m);
   ctx->stats.small_zc_calls++;
@@ -2933,12 +2961,22 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       for (hipEvent_t* e : {&d.ev_longs, &d.ev_join2})
         if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
-    HIPCHK(msha::launch_fold_prefix(fa, ps));
-    if (early) {
-      // the head's stream forks after the prefix (its first decision): the list
-      // runs beside the alias insert
+    // Round 6: the head's stream forks before the tile prefix, right after the
+    // memsets, and makes its first decision itself (k_fold_longs_gate over len);
+    // MSHA_EARLY_FORK=0: after the prefix, which decides (round 5, A/B).
+    fa.early_fork = early && env_u64("MSHA_EARLY_FORK", 1) != 0;
+    if (fa.early_fork) {
       HIPCHK(hipEventRecord(d.ev_longs, ps));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
+    }
+    HIPCHK(msha::launch_fold_prefix(fa, ps));
+    if (early) {
+      // the list runs beside the tile prefix (forked) or after it, and beside the
+      // alias insert
+      if (!fa.early_fork) {
+        HIPCHK(hipEventRecord(d.ev_longs, ps));
+        HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
+      }
       HIPCHK(msha::launch_fold_longs(fa, d.cus, d.head_stream));
       HIPCHK(hipEventRecord(d.ev_longs, d.head_stream));
       msha::LaneGate eg;

@@ -359,7 +359,8 @@ __global__ __launch_bounds__(256) void k_fold_tilemax(FoldArgs a) {
 #pragma unroll
   for (uint32_t r = 0; r < kPlanItems; ++r) m = max(m, o[r]);
   part[threadIdx.x] = m;
-  if (a.long_blocks) {
+  const bool sizes = a.long_blocks && !a.early_fork;  // else k_fold_longs_gate decides
+  if (sizes) {
     uint64_t l[kPlanItems];
     load_run(a.len, base, a.n, a.vec, l);
     uint64_t sum = 0, mx = 0;
@@ -382,7 +383,7 @@ __global__ __launch_bounds__(256) void k_fold_tilemax(FoldArgs a) {
   }
   if (threadIdx.x == 0) {
     a.tmax[blockIdx.x] = part[0];
-    if (a.long_blocks) {
+    if (sizes) {
       a.tsum[2 * blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
       a.tsum[2 * blockIdx.x + 1] = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
     }
@@ -402,16 +403,17 @@ __global__ __launch_bounds__(1024) void k_fold_tilescan(FoldArgs a, uint64_t til
   const uint32_t t = threadIdx.x;
   const uint64_t per = (tiles + 1023) / 1024;
   const uint64_t b0 = min((uint64_t)t * per, tiles), b1 = min(b0 + per, tiles);
+  const bool sizes = a.long_blocks && !a.early_fork;  // else k_fold_longs_gate decides
   uint64_t m = 0, sum = 0, mx = 0;
   for (uint64_t b = b0; b < b1; ++b) {
     m = max(m, a.tmax[b]);
-    if (a.long_blocks) {
+    if (sizes) {
       sum += a.tsum[2 * b];
       mx = max(mx, a.tsum[2 * b + 1]);
     }
   }
   part[t] = m;
-  if (a.long_blocks) {
+  if (sizes) {
     for (uint32_t d = 32; d > 0; d >>= 1) {
       sum += __shfl_xor(sum, d);
       mx = max(mx, (uint64_t)__shfl_xor(mx, d));
@@ -431,7 +433,7 @@ __global__ __launch_bounds__(1024) void k_fold_tilescan(FoldArgs a, uint64_t til
     a.tmax[b] = run;
     run = max(run, v);
   }
-  if (a.long_blocks && t == 0) {
+  if (sizes && t == 0) {
     unsigned long long ss = 0, sm = 0;
     for (int w = 0; w < 16; ++w) ss += s_sum[w], sm = max(sm, s_max[w]);
     const uint64_t t_body = ss * a.wave_block_cycles / (64ull * a.simds);
@@ -914,9 +916,60 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
   }
 }
 
+// The early head's first decision without the tile prefix (FoldArgs::early_fork):
+// one pass over len alone -- the short messages' blocks (the lane kernel's share
+// without the long payloads) and the longest chain -- and the last workgroup to
+// finish decides as k_fold_tilescan would (info[6]). It runs first on the head's
+// stream, forked right after the planner's memsets, beside k_fold_tilemax.
+__global__ __launch_bounds__(256) void k_fold_longs_gate(FoldArgs a) {
+  __shared__ unsigned long long s_sum, s_max;
+  __shared__ bool last;
+  if (threadIdx.x == 0) s_sum = s_max = 0;
+  __syncthreads();
+  uint64_t sum = 0, mx = 0;
+  const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
+  for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const uint64_t base = tile * kPlanTile + (uint64_t)threadIdx.x * kPlanItems;
+    uint64_t l[kPlanItems];
+    load_run(a.len, base, a.n, a.vec, l);
+#pragma unroll
+    for (uint32_t r = 0; r < kPlanItems; ++r) {
+      const uint64_t blocks = base + r < a.n ? dev_blocks_for(l[r]) : 0;
+      mx = max(mx, blocks);
+      if (blocks < a.long_blocks) sum += blocks;
+    }
+  }
+  for (uint32_t d = 32; d > 0; d >>= 1) {  // wave sums, then one LDS atomic per wave
+    sum += __shfl_xor(sum, d);
+    mx = max(mx, (uint64_t)__shfl_xor(mx, d));
+  }
+  if (__lane_id() == 0) {
+    atomicAdd(&s_sum, (unsigned long long)sum);
+    atomicMax(&s_max, (unsigned long long)mx);
+  }
+  __syncthreads();
+  unsigned long long* g = reinterpret_cast<unsigned long long*>(a.info + 12);  // [short blocks, longest]
+  if (threadIdx.x == 0) {
+    atomicAdd(&g[0], s_sum);
+    atomicMax(&g[1], s_max);
+    __threadfence();  // this workgroup's sums before its count
+    last = atomicAdd(&a.info[7], 1u) == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (last && threadIdx.x == 0) {
+    __threadfence();
+    const uint64_t ss = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t sm = __hip_atomic_load(&g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t t_body = ss * a.wave_block_cycles / (64ull * a.simds);
+    const uint64_t t_head = sm * a.early_cycles;
+    a.info[6] = sm >= a.long_blocks && t_body < t_head ? 1u : 0u;
+  }
+}
+
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
   if (a.n == 0 || !a.long_blocks) return hipSuccess;
   const unsigned grid = (unsigned)std::min<uint64_t>((a.n + kPlanTile - 1) / kPlanTile, (uint64_t)cus * 4);
+  if (a.early_fork) hipLaunchKernelGGL(k_fold_longs_gate, dim3(grid), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_longs, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }

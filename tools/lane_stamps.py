@@ -45,13 +45,35 @@ def decode(recs: np.ndarray) -> dict:
     xcc = (recs[:, 4] >> 32).astype(np.int64) & 0xF
     kind = (recs[:, 5] & 0xFFFFFFFF).astype(np.int64)
     block = (recs[:, 5] >> 32).astype(np.int64)
+    work = (recs[:, 6] >> 32).astype(np.int64)
     simd = (hw >> 4) & 3
     cu = (hw >> 8) & 0xF
     sh = (hw >> 12) & 1
     se = (hw >> 13) & 7
     cu_key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
     return {"t0": t0, "r0": r0, "t1": t1, "r1": r1, "kind": kind, "block": block, "cu": cu_key,
-            "simd": cu_key * 4 + simd}
+            "simd": cu_key * 4 + simd, "nb": work & 0xFFFF, "lanes": work >> 16}
+
+
+def simd_busy(simd: np.ndarray, r0: np.ndarray, r1: np.ndarray) -> np.ndarray:
+    """Per SIMD: the union of its waves' [r0, r1) intervals (ticks)."""
+    order = np.lexsort((r0, simd))
+    s, a, b = simd[order], r0[order], r1[order]
+    busy = {}
+    cur_s, cur_a, cur_b, tot = None, 0, 0, 0
+    for k in range(s.size):
+        if s[k] != cur_s:
+            if cur_s is not None:
+                busy[cur_s] = tot + (cur_b - cur_a)
+            cur_s, cur_a, cur_b, tot = s[k], a[k], b[k], 0
+        elif a[k] > cur_b:
+            tot += cur_b - cur_a
+            cur_a, cur_b = a[k], b[k]
+        else:
+            cur_b = max(cur_b, b[k])
+    if cur_s is not None:
+        busy[cur_s] = tot + (cur_b - cur_a)
+    return np.array(list(busy.values()), dtype=np.int64)
 
 
 def summarize(d: dict, step_r0: int, simds_total: int = 1024) -> dict:
@@ -83,6 +105,21 @@ def summarize(d: dict, step_r0: int, simds_total: int = 1024) -> dict:
             ov = np.clip(np.minimum(r1, z) - np.maximum(r0, a), 0, None).sum()
             tl.append(round(float(ov / (z - a) / simds_total), 2))
         e["timeline_waves_per_simd"] = tl
+        e["wave_us_p10_p50_p90_max"] = [float(np.percentile(dr, q)) / 100.0 for q in (10, 50, 90, 100)]
+        if KINDS.get(k) == "lane":
+            nb, lanes = d["nb"][m], d["lanes"][m]
+            busy_ticks = simd_busy(d["simd"][m], r0, r1)
+            clk = e["clock_ghz"] or 2.4
+            # SIMD cycles the waves' SIMDs were busy (any wave resident) per wave-block
+            # (one wave's pass over one block: ~1,356-1,400 VALU instructions, ~5,500
+            # cycles at 4.1 a instruction when the SIMD issues without gaps)
+            e["simd_busy_frac"] = float(busy_ticks.sum() / (span * simds_total))
+            e["wave_blocks"] = int(nb.sum())
+            e["lane_blocks"] = int((nb * lanes).sum())
+            e["busy_simd_cycles_per_wave_block"] = float(busy_ticks.sum() / 100.0 * 1e3 * clk / max(1, nb.sum()))
+            e["full_lane_share"] = float(lanes.sum() / max(1, 64 * (nb > 0).sum()))
+            e["blocks_per_wave_hist"] = {int(b): int(c) for b, c in zip(*np.unique(nb, return_counts=True))
+                                         if c >= max(1, m.sum() // 200)}
         out[KINDS.get(k, str(k))] = e
     return out
 
@@ -143,6 +180,10 @@ def main():
         k = int(recs.shape[0])
         d = decode(recs)
         step_r0 = int(d["r0"].min())
+        raw = os.environ.get("RAW_DIR")
+        if raw:
+            os.makedirs(raw, exist_ok=True)
+            np.savez_compressed(os.path.join(raw, f"stamps_{form}.npz"), recs=recs)
         line = {"form": form, "workload": w.name, "library": _lib.build_id()["id"], "kernel": kind,
                 "step_ms_stamped_build": step_ms, "records": k,
                 "hashed_blocks": bench.hashed_blocks(w, form),
