@@ -50,7 +50,7 @@ __device__ uint32_t* g_wave_stamp_count;  // [1]: records per kind (the buffer h
 struct WaveStamp {
   uint64_t t0, r0;
   __device__ __forceinline__ WaveStamp() : t0(__builtin_amdgcn_s_memtime()), r0(__builtin_amdgcn_s_memrealtime()) {}
-  __device__ __forceinline__ void close(uint32_t kind, uint32_t nb = 0) {
+  __device__ __forceinline__ void close(uint32_t kind, uint32_t nb = 0, uint64_t at = ~0ull) {
     const uint64_t t1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
     uint32_t mx = nb;
     for (int d = 32; d > 0; d >>= 1) mx = max(mx, (uint32_t)__shfl_xor((int)mx, d));
@@ -59,7 +59,7 @@ struct WaveStamp {
     // a fixed slot per (kind, wave): a shared counter's returning atomic at every
     // wave's end queued the waves behind it (c2's stamped step ran 2.3x longer)
     const uint32_t per = g_wave_stamp_count[1];
-    const uint64_t w = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const uint64_t w = at != ~0ull ? at : (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (w >= per) return;
     const uint64_t k = (uint64_t)(kind - 1) * per + w;
     WaveStampRec r;
@@ -80,6 +80,7 @@ struct WaveStamp {
 #define MSHA_WAVE_STAMP_OPEN() WaveStamp wave_stamp_;
 #define MSHA_WAVE_STAMP_CLOSE(kind) wave_stamp_.close(kind);
 #define MSHA_WAVE_STAMP_CLOSE_NB(kind, nb) wave_stamp_.close(kind, nb);
+#define MSHA_WAVE_STAMP_CLOSE_AT(kind, nb, at) wave_stamp_.close(kind, nb, at);
 }  // namespace msha
 // Diagnostic build only: points the stamps at `buf` (device memory, 5 x per
 // records of 64 B: one region per StampKind, a wave's record at its wave index)
@@ -98,6 +99,7 @@ namespace msha {
 #define MSHA_WAVE_STAMP_OPEN()
 #define MSHA_WAVE_STAMP_CLOSE(kind)
 #define MSHA_WAVE_STAMP_CLOSE_NB(kind, nb)
+#define MSHA_WAVE_STAMP_CLOSE_AT(kind, nb, at)
 #endif
 
 template <int MODE = 0>
@@ -360,6 +362,101 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch(const uint8_t* __restri
   const uint64_t l1 = digest_batch_lane<MODE>(arena, off, len, order, out_idx, n, out, err, skip_below);
   MSHA_WAVE_STAMP_CLOSE_NB(kStampLane, l1 ? (uint32_t)((l1 - 1) >> 6) + ((((l1 - 1) & 63) < 56) ? 1u : 2u) : 0u)
   (void)l1;
+}
+
+// ---------------------------------------------------------------------------
+// The lane kernel with work stealing (round 6, VERDICT r5 item 1: folded c5's lane
+// kernel ran at 0.465 of the peak against c2's 0.502 with equal instructions and
+// cycles per instruction). Wave stamps of a folded step (tools/lane_stamps.py,
+// profiles/r06_xcd/) showed why: a launch's workgroups go to the XCDs by blockIdx
+// mod 8, and an XCD that also holds a long-lived wave -- the late head's chain
+// (2 ms), or a 652-block chain left on the lane kernel -- dispatches its lane
+// workgroups at ~3 resident waves per SIMD instead of 8, so its fixed eighth of
+// the lanes ends ~250 us after the other XCDs' while they idle (SIMDs busy 91 %
+// of the span, against 98 % on c2; cycles per wave-block while busy equal).
+// Here a grid of resident workgroups (8 a CU) takes 64-lane tiles from kWsSlots
+// counters: slot s owns the tiles t = s + kWsSlots k, so every slot holds the same
+// mix of classes (descending, as the lanes are ordered), and workgroup b starts on
+// slot b mod kWsSlots (the same XCD as b). A wave whose slot is used up looks at
+// every other slot at once (one counter a lane, agent-scope loads) and takes a
+// tile from the first with some left. Nothing is dispatched after the start, so a
+// throttled dispatcher costs nothing but its few late workgroups, and an XCD that
+// runs slow takes fewer tiles. 64 counters, 64 bytes apart: eight (one an XCD)
+// serialised ~2.3 M claims/s each and ran folded c5 at 7 ms (profiles/r06_ws/).
+// Termination: a claim past a slot's count proves the slot used up (counters only
+// grow), and the scan's loads are coherent, so each wave fails on a slot at most
+// once and leaves when no slot has tiles left.
+// ctr: kWsSlots x kWsStride zeroed words (the planner's memset); lanes_dev (may be
+// null): a device count of the positions worth visiting (the planner's lanes: the
+// kNoLane tail past it is never claimed).
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256, 8) void k_digest_batch_ws(const uint8_t* __restrict__ arena,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint64_t* __restrict__ len,
+                                                         const uint32_t* __restrict__ order,
+                                                         const uint32_t* __restrict__ out_idx, uint64_t n,
+                                                         uint8_t* __restrict__ out, uint32_t* __restrict__ err,
+                                                         const uint32_t* __restrict__ skip_below,
+                                                         uint32_t* __restrict__ ctr,
+                                                         const uint32_t* __restrict__ lanes_dev) {
+  static_assert(kWsSlots == 64, "the steal scan gives each lane one slot");
+  const uint64_t n_eff = lanes_dev ? min(n, (uint64_t)*lanes_dev) : n;
+  const uint32_t tiles = (uint32_t)((n_eff + 63) / 64);
+  const unsigned lane = threadIdx.x & 63;
+  uint32_t slot = blockIdx.x % kWsSlots;
+  for (;;) {
+    const uint32_t cnt = slot < tiles ? (tiles - 1 - slot) / kWsSlots + 1 : 0;
+    uint32_t* c = ctr + slot * kWsStride;
+    uint32_t k = cnt;
+    if (lane == 0 && __hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < cnt) k = atomicAdd(c, 1u);
+    k = __builtin_amdgcn_readfirstlane(k);
+    if (k >= cnt) {  // used up: the slots with tiles left, one per lane
+      const uint32_t s2 = (slot + 1 + lane) % kWsSlots;
+      const uint32_t c2 = s2 < tiles ? (tiles - 1 - s2) / kWsSlots + 1 : 0;
+      const bool left = __hip_atomic_load(ctr + s2 * kWsStride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < c2;
+      const uint64_t any = __ballot(left);
+      if (!any) break;
+      slot = __builtin_amdgcn_readfirstlane(__shfl(s2, __ffsll((long long)any) - 1));
+      continue;
+    }
+    const uint32_t t = k * kWsSlots + slot;
+    MSHA_WAVE_STAMP_OPEN()
+    const uint64_t i = (uint64_t)t * 64 + lane;
+    uint64_t l1 = 0;
+    uint64_t m = i;
+    bool live = i < n_eff && !(skip_below && i < *skip_below);
+    if (live && order) {
+      const uint32_t v = order[i];
+      live = v != kNoLane;
+      m = v;
+    }
+    const uint64_t l = live ? len[m] : 0;
+    // Issue priority by the tile's longest chain. A statically mapped launch
+    // dispatches its longest lanes first, and the SIMD's oldest-first issue then
+    // runs those chains nearly alone; resident waves are all the same age, so
+    // without this a long chain shared its SIMD evenly with short tiles and ended
+    // last (unfolded c5 13.3 -> 20.8 ms, profiles/r06_ws/).
+    uint32_t nb = live ? (uint32_t)(l >> 6) + ((l & 63) < 56 ? 1u : 2u) : 0u;
+    for (int d = 32; d > 0; d >>= 1) nb = max(nb, (uint32_t)__shfl_xor((int)nb, d));
+    nb = __builtin_amdgcn_readfirstlane(nb);
+    if (nb >= 256)
+      __builtin_amdgcn_s_setprio(3);
+    else if (nb >= 48)
+      __builtin_amdgcn_s_setprio(2);
+    else if (nb >= 16)
+      __builtin_amdgcn_s_setprio(1);
+    else
+      __builtin_amdgcn_s_setprio(0);
+    if (live) {
+      const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;
+      const uint8_t* p = arena + off[m];
+      if (check_aligned(p, out + 32 * o, err)) hash_message<MODE>(p, l, out + 32 * o);
+      l1 = l + 1;
+    }
+    MSHA_WAVE_STAMP_CLOSE_AT(kStampLane, l1 ? (uint32_t)((l1 - 1) >> 6) + ((((l1 - 1) & 63) < 56) ? 1u : 2u) : 0u, t)
+    (void)l1;
+  }
 }
 
 // k_digest_batch with the pipelined message loop; no occupancy hint (one wave
@@ -1747,19 +1844,24 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
   if (n == 0) return hipSuccess;
   const uint32_t* head = gate ? gate->head : nullptr;
   if (gate && gate->head_part) {  // the planned launch's long chains, up to *head
+#ifdef MSHA_HEAD_NO_EXCL  // A/B build (tools/r06_xcd.sh): heads share their CUs, normal priority
+    constexpr bool kX = false;
+#else
+    constexpr bool kX = true;
+#endif
     if (gate->eight_lane) {
       const unsigned grid = (unsigned)((n + kChain8MsgsPerWg - 1) / kChain8MsgsPerWg);
-      hipLaunchKernelGGL((k_digest_chain8<kPrefetch, true>), dim3(grid), dim3(256), 0, st, arena, off, len,
+      hipLaunchKernelGGL((k_digest_chain8<kPrefetch, kX>), dim3(grid), dim3(256), 0, st, arena, off, len,
                          order, out_idx, n, out, err, head);
       set_kind(kind, kLaunchChain8);
     } else if (gate->two_lane) {
       const unsigned grid = (unsigned)((n + kChain2MsgsPerWg - 1) / kChain2MsgsPerWg);
-      hipLaunchKernelGGL((k_digest_chain2<kPrefetch, true>), dim3(grid), dim3(192), 0, st, arena, off, len,
+      hipLaunchKernelGGL((k_digest_chain2<kPrefetch, kX>), dim3(grid), dim3(192), 0, st, arena, off, len,
                          order, out_idx, n, out, err, head);
       set_kind(kind, kLaunchChain2);
     } else {
       const unsigned grid = (unsigned)((n + kCoopMsgsPerWg - 1) / kCoopMsgsPerWg);
-      hipLaunchKernelGGL((k_digest_coop<kPrefetch, true>), dim3(grid), dim3(256), kCoopDynLds, st, arena, off,
+      hipLaunchKernelGGL((k_digest_coop<kPrefetch, kX>), dim3(grid), dim3(256), kCoopDynLds, st, arena, off,
                          len, order, out_idx, n, out, err, head);
       set_kind(kind, kLaunchCoop);
     }
@@ -1809,6 +1911,15 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
     hipLaunchKernelGGL(k_digest_batch_pipe, dim3(grid_for(n)), dim3(256), 0, st, arena, off, len,
                        order, out_idx, n, out, err, head);
     set_kind(kind, kLaunchPipe);
+    return hipGetLastError();
+  }
+  if (gate && gate->ws_ctr) {  // resident workgroups stealing 64-lane tiles (k_digest_batch_ws)
+    const unsigned grid = (unsigned)std::min<uint64_t>((uint64_t)cus * 8, (n + 255) / 256);
+    with_mode(mode, [&](auto m) {
+      hipLaunchKernelGGL(k_digest_batch_ws<decltype(m)::value>, dim3(grid), dim3(256), 0, st, arena, off, len,
+                         order, out_idx, n, out, err, head, gate->ws_ctr, gate->lanes);
+    });
+    set_kind(kind, kLaunchLane);
     return hipGetLastError();
   }
   with_mode(mode, [&](auto m) {

@@ -44,11 +44,17 @@ enum LaunchKind { kLaunchNone = 0, kLaunchLane, kLaunchPipe, kLaunchCoop, kLaunc
 // over the whole order either is that head (head_part: cooperative, lanes at or
 // past *head idle) or the rest (lanes below *head idle); neither splits.
 constexpr uint32_t kNoLane = 0xFFFFFFFFu;
+constexpr uint32_t kWsSlots = 64, kWsStride = 16;  // work-stealing tile counters, 64 B apart
 struct LaneGate {
   const uint32_t* head = nullptr;
   bool head_part = false;
   bool two_lane = false;  // head_part: k_digest_chain2 instead of the cooperative kernel
   bool eight_lane = false;  // head_part: k_digest_chain8 (eight lanes a message, 24 a CU)
+  // the body (not head_part): kWsSlots x kWsStride zeroed device words -> the
+  // work-stealing lane kernel (k_digest_batch_ws), with `lanes` (device, may be
+  // null) the positions worth visiting
+  uint32_t* ws_ctr = nullptr;
+  const uint32_t* lanes = nullptr;
 };
 
 hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const uint64_t* len,
@@ -181,6 +187,10 @@ struct FoldArgs {
   // alone, then k_fold_longs), so the head's chain does not wait for the prefix;
   // k_fold_tilemax / k_fold_tilescan then size only the offsets.
   uint32_t early_fork = 0;
+  // Round 6: with the work-stealing lane kernel (k_digest_batch_ws) the head's cut
+  // keeps every lane of at least ws_long blocks off the lane kernel when it can
+  // (a long chain there shares a SIMD with same-age waves: kernels.hip); 0: off.
+  uint32_t ws_long = 0;
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;

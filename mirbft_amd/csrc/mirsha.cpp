@@ -2844,7 +2844,9 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     while (cap < 2 * n) cap <<= 1;
     // one zeroed block: info (12 words, padded to 64 bytes), the bucket counters,
     // then FoldArgs::big -- cleared by ONE memset per call
-    const uint64_t fold_zero = 64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets;
+    // (+ the work-stealing lane kernel's tile counters)
+    const uint64_t fold_zero = 64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets +
+                               4 * msha::kWsSlots * msha::kWsStride;
     d.f_cnt.ensure(fold_zero);
     d.f_key.ensure(2 * n);
     d.f_tkeys.ensure(8 * n + 4 * ((n + 4095) / 4096) + 8 * 4096);  // per-tile key lists, then their counts
@@ -2940,6 +2942,13 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.early_cycles = eight_lane ? 3250 : 3500;  // eight-lane: 1,427 blocks in 1.93 ms at ~2.4 GHz (r05)
     fa.tiebreak = (uint32_t)env_u64("MSHA_PLAN_TIEBREAK", 1);
     fa.race_test = (uint32_t)env_u64("MSHA_FOLD_LONGS_SKIP_ODD", 0);
+    // The lane kernel of a folded call steals work (k_digest_batch_ws: folded c5
+    // 2.79 -> 2.69 ms, profiles/r06_ws/); an unfolded one keeps the statically
+    // mapped kernel, whose oldest-first issue runs a storm's thousands of long
+    // chains one after another (work stealing: 13.3 -> 17.6 ms). MSHA_LANE_WS:
+    // 0 never, 2 always (A/B).
+    const uint64_t lane_ws = env_u64("MSHA_LANE_WS", 1);
+    fa.ws_long = !all_coop && (lane_ws == 2 || (lane_ws == 1 && fold)) ? 64u : 0u;
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
     fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);
@@ -3001,6 +3010,13 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     } else {
       msha::LaneGate body;
       body.head = fa.info + 1;
+      // Round 6: the body on the work-stealing lane kernel (kernels.hip
+      // k_digest_batch_ws), over the planned lanes only (fa.ws_long, set before
+      // the plan: the cut then keeps long chains off it)
+      if (fa.ws_long) {
+        body.ws_ctr = reinterpret_cast<uint32_t*>(fa.big + 2 * msha::kFoldBigBuckets);
+        body.lanes = fa.info;
+      }
       if (head) {
         HIPCHK(hipEventRecord(d.ev_fplan, d.side_stream));
         msha::LaneGate hg;

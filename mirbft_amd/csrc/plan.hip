@@ -688,7 +688,10 @@ __device__ __forceinline__ uint64_t head_cost(const FoldArgs& a, uint64_t h, uin
   const uint64_t t_head = h ? max_blocks * a.coop_cycles / 100 * a.head_pct : 0;
   const uint64_t t_body = (btot - bh) * a.wave_block_cycles / (64ull * 4 * (cus - hcus));
   const uint64_t t_lanes = max(t_body, next_blocks * a.lane_cycles);
-  return max(t_head, t_lanes) + (a.tiebreak ? t_lanes / 8 : 0);
+  // work-stealing lane kernel: a cut that leaves a long chain on it loses to any
+  // that does not (FoldArgs::ws_long)
+  const uint64_t ws_penalty = a.ws_long && next_blocks >= a.ws_long ? (1ull << 36) : 0;
+  return max(t_head, t_lanes) + (a.tiebreak ? t_lanes / 8 : 0) + ws_penalty;
 }
 
 constexpr uint64_t kCostMax = (uint64_t(1) << 40) - 1;
