@@ -328,9 +328,10 @@ def kind_of(st0: dict, st1: dict) -> str:
     (the chain kernels are counted in launches_coop too: "coop" names only the
     cooperative kernel itself)."""
     d = {k: st1[k] - st0[k] for k in ("launches_lane", "launches_pipe", "launches_coop", "launches_split",
-                                      "launches_dod", "launches_chain2", "launches_chain8")}
+                                      "launches_dod", "launches_chain2", "launches_chain8", "launches_lane_ws")}
     d["launches_coop"] -= d["launches_chain2"] + d["launches_chain8"]
-    names = {"launches_lane": "lane", "launches_pipe": "pipe", "launches_coop": "coop",
+    d["launches_lane"] -= d["launches_lane_ws"]
+    names = {"launches_lane": "lane", "launches_lane_ws": "lane_ws", "launches_pipe": "pipe", "launches_coop": "coop",
              "launches_chain2": "chain2", "launches_chain8": "chain8",
              "launches_split": "split", "launches_dod": "digest_of_digests"}
     ran = [v for k, v in names.items() if d[k] > 0]

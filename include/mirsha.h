@@ -97,6 +97,8 @@ typedef struct {
   uint64_t launches_chain8; /* eight lanes a message (k_digest_chain8): the folded early head, small launches */
   uint64_t small_zc_calls;  /* of small_calls, those served zero-copy: the kernel read the packed list and wrote
                                the digests in coherent pinned memory, no H2D or D2H (ABI 10) */
+  uint64_t launches_lane_ws; /* of launches_lane, the work-stealing lane kernel (k_digest_batch_ws: folded
+                                planned calls; ABI 10) */
 } msha_stats;
 
 /* Per-GPU figures of the last host-memory call (one entry per shard; a shard is

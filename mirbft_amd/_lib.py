@@ -63,6 +63,7 @@ class MshaStats(ctypes.Structure):
         ("launches_chain2", ctypes.c_uint64),
         ("launches_chain8", ctypes.c_uint64),
         ("small_zc_calls", ctypes.c_uint64),
+        ("launches_lane_ws", ctypes.c_uint64),
     ]
 
 

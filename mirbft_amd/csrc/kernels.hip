@@ -1919,7 +1919,7 @@ hipError_t launch_digest_batch(const uint8_t* arena, const uint64_t* off, const 
       hipLaunchKernelGGL(k_digest_batch_ws<decltype(m)::value>, dim3(grid), dim3(256), 0, st, arena, off, len,
                          order, out_idx, n, out, err, head, gate->ws_ctr, gate->lanes);
     });
-    set_kind(kind, kLaunchLane);
+    set_kind(kind, kLaunchLaneWs);
     return hipGetLastError();
   }
   with_mode(mode, [&](auto m) {

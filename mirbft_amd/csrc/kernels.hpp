@@ -34,8 +34,9 @@ bool plan_split(uint64_t n, int cus, int policy, SplitPlan* sp, int cap);
 
 // Which kernel a launcher ran (msha_stats launch counters; tests assert them).
 // kLaunchChain2 / kLaunchChain8 count as cooperative launches too (launches_coop).
+// kLaunchLaneWs (the work-stealing lane kernel) counts as a lane launch too.
 enum LaunchKind { kLaunchNone = 0, kLaunchLane, kLaunchPipe, kLaunchCoop, kLaunchSplit, kLaunchDod,
-                  kLaunchChain2, kLaunchChain8 };
+                  kLaunchChain2, kLaunchChain8, kLaunchLaneWs };
 
 // GPU-planned device launches (plan.hip: msha_digest_batch_device_planned). The
 // planner's lane order holds kNoLane at positions it leaves unused (folded
@@ -191,6 +192,7 @@ struct FoldArgs {
   // keeps every lane of at least ws_long blocks off the lane kernel when it can
   // (a long chain there shares a SIMD with same-age waves: kernels.hip); 0: off.
   uint32_t ws_long = 0;
+  uint32_t longs_wgs = 0;  // k_fold_longs / k_fold_longs_gate workgroups (0: 4 a CU; A/B MSHA_LONGS_WGS)
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;

@@ -622,6 +622,10 @@ void count_launch(msha_ctx* ctx, Device* d, msha::LaunchKind kind) {
       f = &ctx->stats.launches_coop;
       __atomic_fetch_add(&ctx->stats.launches_chain8, 1, __ATOMIC_RELAXED);
       break;
+    case msha::kLaunchLaneWs:
+      f = &ctx->stats.launches_lane;
+      __atomic_fetch_add(&ctx->stats.launches_lane_ws, 1, __ATOMIC_RELAXED);
+      break;
     default: return;
   }
   __atomic_fetch_add(f, 1, __ATOMIC_RELAXED);
@@ -2948,7 +2952,13 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // chains one after another (work stealing: 13.3 -> 17.6 ms). MSHA_LANE_WS:
     // 0 never, 2 always (A/B).
     const uint64_t lane_ws = env_u64("MSHA_LANE_WS", 1);
-    fa.ws_long = !all_coop && (lane_ws == 2 || (lane_ws == 1 && fold)) ? 64u : 0u;
+    const bool ws = !all_coop && (lane_ws == 2 || (lane_ws == 1 && fold));
+    // MSHA_WS_LONG=k (A/B): the cut also keeps chains of >= k blocks off it. Every
+    // k tried lost to the cost model alone, which takes fewer head CUs (folded c5,
+    // 3 reps: 2.661-2.669 ms; k = 600 / 256 / 64: 2.715-2.719 / 2.709-2.744 /
+    // 2.725-2.736; static lane kernel 2.78-2.89; profiles/r06_ws2/)
+    const uint64_t ws_long_env = env_u64("MSHA_WS_LONG", 0);
+    fa.ws_long = ws ? (ws_long_env ? (uint32_t)std::min<uint64_t>(ws_long_env, 0xFFFFFFFFull) : 0xFFFFFFFFu) : 0u;
     fa.head_pct = (uint32_t)env_u64("MSHA_PLAN_HEAD_PCT", 100);
     fa.lane_cycles = (uint32_t)env_u64("MSHA_PLAN_LANE_CYCLES", fa.lane_cycles);  // A/B of the cost model
     fa.wave_block_cycles = (uint32_t)env_u64("MSHA_PLAN_WAVE_CYCLES", fa.wave_block_cycles);
@@ -2970,10 +2980,13 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       for (hipEvent_t* e : {&d.ev_longs, &d.ev_join2})
         if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
-    // Round 6: the head's stream forks before the tile prefix, right after the
-    // memsets, and makes its first decision itself (k_fold_longs_gate over len);
-    // MSHA_EARLY_FORK=0: after the prefix, which decides (round 5, A/B).
-    fa.early_fork = early && env_u64("MSHA_EARLY_FORK", 1) != 0;
+    // Round 6 A/B (MSHA_EARLY_FORK=1): the head's stream forks before the tile
+    // prefix, right after the memsets, and makes its first decision itself
+    // (k_fold_longs_gate over len). The chain then starts ~13 us sooner over 8
+    // GPUs with no measurable step change, and one GPU lost ~27 us (the gate's
+    // pass beside the prefix): off by default (profiles/r06_call4/).
+    fa.early_fork = early && env_u64("MSHA_EARLY_FORK", 0) != 0;
+    fa.longs_wgs = (uint32_t)env_u64("MSHA_LONGS_WGS", 0);
     if (fa.early_fork) {
       HIPCHK(hipEventRecord(d.ev_longs, ps));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));

@@ -971,7 +971,10 @@ __global__ __launch_bounds__(256) void k_fold_longs_gate(FoldArgs a) {
 
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
   if (a.n == 0 || !a.long_blocks) return hipSuccess;
-  const unsigned grid = (unsigned)std::min<uint64_t>((a.n + kPlanTile - 1) / kPlanTile, (uint64_t)cus * 4);
+  // a.longs_wgs (A/B): fewer workgroups, fewer of the same-address atomics that end
+  // each one (each costs ~20 ns serialised: profiles/r06_call4/)
+  const uint64_t cap = a.longs_wgs ? a.longs_wgs : (uint64_t)cus * 4;
+  const unsigned grid = (unsigned)std::min<uint64_t>((a.n + kPlanTile - 1) / kPlanTile, cap);
   if (a.early_fork) hipLaunchKernelGGL(k_fold_longs_gate, dim3(grid), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_longs, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();

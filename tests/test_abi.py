@@ -180,7 +180,7 @@ def test_stats_and_shard_stats_null_args():
     assert lib.msha_shard_count(None, ctypes.byref(n)) == L.MSHA_ERR_INVALID_ARG
     assert lib.msha_get_shard_stats(None, 0, None) == L.MSHA_ERR_INVALID_ARG
     assert ctypes.sizeof(L.MshaShardStats) == 8 * 15
-    assert ctypes.sizeof(L.MshaStats) == 8 * 23
+    assert ctypes.sizeof(L.MshaStats) == 8 * 24
 
 
 def _first_ref(off, ln):
@@ -294,7 +294,7 @@ def test_stats_structs_match_the_header(tmp_path):
     import ctypes
     import subprocess
     src = tmp_path / "layout.c"
-    names = {"msha_stats": (L.MshaStats, "small_zc_calls"), "msha_shard_stats": (L.MshaShardStats, "plan_kernel_ms"),
+    names = {"msha_stats": (L.MshaStats, "launches_lane_ws"), "msha_shard_stats": (L.MshaShardStats, "plan_kernel_ms"),
              "msha_clock_info": (L.MshaClockInfo, "blocks_per_lane")}
     body = "".join('printf("%%s %%zu %%zu\\n", "%s", sizeof(%s), offsetof(%s, %s));\n' % (n, n, n, last)
                    for n, (_, last) in names.items())

@@ -41,6 +41,12 @@ def _early(fold):
             and os.environ.get("MSHA_HEAD_CHAIN2", "1") != "0")
 
 
+def _ws(fold):
+    """Does a planned call's lane kernel steal work (MSHA_LANE_WS: 1 folded calls, 2 all, 0 none)?"""
+    v = os.environ.get("MSHA_LANE_WS", "1")
+    return v == "2" or (v == "1" and fold)
+
+
 def _chain8():
     """Does the early head run on the eight-lane kernel (k_digest_chain8)?"""
     return os.environ.get("MSHA_HEAD_CHAIN8", "1") != "0"
@@ -86,6 +92,8 @@ def test_c5_full_size_planned(engine, fold):
     assert np.array_equal(got, exp)
     assert _delta(before, after, "planned_device_calls") == 1
     assert _delta(before, after, "launches_lane") == 1     # one lane launch over the whole order
+    # folded: the work-stealing lane kernel (k_digest_batch_ws); unfolded: the static one
+    assert _delta(before, after, "launches_lane_ws") == (1 if _ws(fold) else 0)
     torch.cuda.empty_cache()
 
 
@@ -209,6 +217,32 @@ def test_empty_and_boundary_lengths(engine):
     exp = _expect(w)
     for fold in (False, True):
         assert np.array_equal(_run(engine, w, fold), exp)
+
+
+@pytest.mark.parametrize("ws", ["0", "2"])
+@pytest.mark.parametrize("seed", range(4))
+def test_fuzz_lane_kernels(engine, monkeypatch, seed, ws):
+    """The static and the work-stealing lane kernels forced either way (MSHA_LANE_WS=0:
+    static everywhere, 2: work stealing on unfolded calls too), over batches whose lane
+    counts are not multiples of a tile, with long chains left on the lane kernel, heads
+    and folded tails: every digest exact, the kernel counted."""
+    monkeypatch.setenv("MSHA_LANE_WS", ws)
+    rng = np.random.default_rng(7000 + seed)
+    n = int(rng.choice([40_001, 77_777, 150_000, 300_003]))
+    ln = rng.integers(0, 1200, n).astype(np.uint64)
+    big = rng.random(n) < 0.002
+    ln[big] = rng.integers(20_000, 200_000, int(big.sum())).astype(np.uint64)
+    off, arena = _packed(ln, 0x7000 + seed)
+    if seed % 2:  # 20 % alias an earlier message (folded tails of kNoLane positions)
+        src = rng.integers(0, n, n)
+        al = (rng.random(n) < 0.2) & (src < np.arange(n))
+        off[al], ln[al] = off[src[al]], ln[src[al]]
+    w = W.Workload(f"lanefuzz{seed}", arena, off, ln)
+    exp = _expect(w, 8)
+    for fold in (False, True):
+        before = engine.stats()
+        assert np.array_equal(_run(engine, w, fold), exp)
+        assert _delta(before, engine.stats(), "launches_lane_ws") == (1 if _ws(fold) else 0)
 
 
 @pytest.mark.parametrize("seed", range(12))

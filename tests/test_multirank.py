@@ -101,8 +101,9 @@ def test_bench_two_ranks_on_the_engine():
         f = d["extra_configs"][form]
         assert f["n_gpus"] == 2 and f["scaling"] == "strong" and f["value"] > 0 and f["blocks"] == c5["blocks"]
         assert "512 digests per rank" in f["verified"]
-        # unfolded: the cooperative head; folded: the late head on the two-lane chain, the early one on eight
-        assert f["kernel"] == {"c5_planned": "lane+coop", "c5_folded": "lane+chain2+chain8"}[form], f["kernel"]
+        # unfolded: the cooperative head; folded: the work-stealing lane kernel, the late head on the
+        # two-lane chain, the early one on eight
+        assert f["kernel"] == {"c5_planned": "lane+coop", "c5_folded": "lane_ws+chain2+chain8"}[form], f["kernel"]
     assert d["extra_configs"]["c5_folded"]["hashed_blocks"] < c5["blocks"] == d["extra_configs"]["c5_planned"]["hashed_blocks"]
     # the CPU baseline at N > 1 too (rank 0, after the ranks released their GPUs)
     cb = d["cpu_baseline"]
