@@ -1158,8 +1158,12 @@ struct SmallSpan {
 // and the digests are written straight into coherent pinned memory: one launch and
 // one synchronize per call. The packer's own 16-byte aligned offsets cannot raise
 // the device error word (check_aligned), so it stays on the device.
-uint64_t small_zc_bytes() { return env_u64("MSHA_SMALL_ZC_BYTES", 64ull << 10); }  // 0 disables
-uint64_t small_zc_msgs(const Device& d) { return std::min<uint64_t>(env_u64("MSHA_SMALL_ZC_MSGS", 256),
+// Limits measured per call (tools/latency.cpp, profiles/r06_latency/): 512-B
+// requests zero-copy / copying, 1: 29.6 / 38.1 us, 64: 31.7 / 42.0, 256: 33.9 /
+// 46.8, 1,024: 47.9 / 70.5, 4,096: 108.1 / 111.2 (the kernel's PCIe reads then cost
+// what the copy saved).
+uint64_t small_zc_bytes() { return env_u64("MSHA_SMALL_ZC_BYTES", 1ull << 20); }  // 0 disables
+uint64_t small_zc_msgs(const Device& d) { return std::min<uint64_t>(env_u64("MSHA_SMALL_ZC_MSGS", 2048),
                                                                     (uint64_t)d.cus * msha::kChain8MsgsPerWg); }
 
 template <class Fill>

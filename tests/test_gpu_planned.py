@@ -239,10 +239,14 @@ def test_fuzz_lane_kernels(engine, monkeypatch, seed, ws):
         off[al], ln[al] = off[src[al]], ln[src[al]]
     w = W.Workload(f"lanefuzz{seed}", arena, off, ln)
     exp = _expect(w, 8)
+    import torch
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
     for fold in (False, True):
         before = engine.stats()
         assert np.array_equal(_run(engine, w, fold), exp)
-        assert _delta(before, engine.stats(), "launches_lane_ws") == (1 if _ws(fold) else 0)
+        # at most one wave per SIMD the pipelined kernel runs instead (kernels.hip pick_mode)
+        ws_ran = _ws(fold) and n > cus * 4 * 64
+        assert _delta(before, engine.stats(), "launches_lane_ws") == int(ws_ran), (n, fold)
 
 
 @pytest.mark.parametrize("seed", range(12))

@@ -7,8 +7,10 @@ rocprofv3 kernel summaries of the same configs and the PMC summary:
 
 One markdown row per config: digests/s, GB/s hashed, the mean launch from the
 line's HIP events beside rocprofv3's average for the dominant kernel, roofline
-frac (at 78.64 T and at the line's own effective clock), the PMC pass's VALU
-busy, SIMD cycles per VALU instruction and HBM bytes over the algorithmic ones."""
+frac (at 78.64 T), the PMC pass's VALU busy, SIMD cycles per VALU instruction
+and HBM bytes over the algorithmic ones. No fraction "at a clock" is printed: the
+only clocks are the PMC-counted one and a probe kernel's after the timed steps
+(round 6: the in-kernel stamps of tools/lane_stamps.py are the clock evidence)."""
 import csv
 import json
 import os
@@ -33,13 +35,12 @@ def main():
     bench, prof_dir, pmc_path = sys.argv[1:4]
     line = json.load(open(bench))
     pmc = json.load(open(pmc_path))["configs"]
-    legs = {"c2": dict(line, frac=line["roofline"]["frac"], frac_at_clock=line["roofline"]["frac_at_clock"],
-                       traffic=line["roofline"]["traffic"])}
+    legs = {"c2": dict(line, frac=line["roofline"]["frac"], traffic=line["roofline"]["traffic"])}
     legs.update(line.get("extra_configs", {}))
-    print("| config | kernel | digests/s | GB/s hashed | mean launch (default line) | rocprof command: events / "
-          "rocprof avg | roofline.frac (at the line's clock) | clock GHz | VALU busy | SIMD cycles / VALU instr | "
+    print("| config | dominant kernel (launches in the line) | digests/s | GB/s hashed | mean launch (default line) | "
+          "rocprof command: events / rocprof avg | roofline.frac | VALU busy | SIMD cycles / VALU instr | "
           "HBM ÷ algorithmic |")
-    print("|---|---|---|---|---|---|---|---|---|---|---|")
+    print("|---|---|---|---|---|---|---|---|---|---|")
     for cfg, leg in legs.items():
         p = pmc.get(PMC_NAME.get(cfg, ""), {})
         kern = p.get("kernel", "")
@@ -54,9 +55,9 @@ def main():
 
         def f(v, fmt, suffix=""):  # a figure the PMC summary left null (unresolved clock) prints as a dash
             return format(v, fmt) + suffix if isinstance(v, (int, float)) else "—"
-        print(f"| {cfg} | `{short}` | {leg['value'] / 1e9:.3g} G | {leg['gbps_hashed']:,.0f} | "
-              f"{ev_us:,.1f} µs | {own_s} / {rp_s} µs | {leg['frac']:.3f} ({f(leg.get('frac_at_clock'), '.3f')}) | "
-              f"{f(leg.get('effective_clock_ghz'), '.2f')} | {f(p.get('valu_busy_pct'), '.1f', ' %')} | "
+        print(f"| {cfg} | `{short}` ({leg.get('kernel', '')}) | {leg['value'] / 1e9:.3g} G | {leg['gbps_hashed']:,.0f} | "
+              f"{ev_us:,.1f} µs | {own_s} / {rp_s} µs | {leg['frac']:.3f} | "
+              f"{f(p.get('valu_busy_pct'), '.1f', ' %')} | "
               f"{f(p.get('simd_cycles_per_valu_instr'), '.2f')} | {f(hbm, '.2f', '×')} |")
 
 if __name__ == "__main__":
