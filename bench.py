@@ -200,7 +200,7 @@ def cpu_baseline(w, seconds: float):
     return line
 
 
-PMC_FILE = "profiles/r05_pmc.json"          # tools/pmc_valu.sh -> tools/pmc_summary.py, this round's code
+PMC_FILE = "profiles/r06_pmc.json"          # tools/pmc_valu.sh -> tools/pmc_summary.py, this round's code
 
 
 def measured_traffic(cfg: str):

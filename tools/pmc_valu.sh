@@ -8,7 +8,7 @@
 #    python3 tools/pmc_summary.py gpurun_out/pmc profiles/r04_pmc.json
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/pmc
+OUT=${OUT:-gpurun_out/pmc}
 mkdir -p $OUT
 prof() {  # name, counters, cmd...
   local name=$1 ctr=$2; shift 2
