@@ -405,6 +405,10 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch_ws(const uint8_t* __res
   const uint32_t tiles = (uint32_t)((n_eff + 63) / 64);
   const unsigned lane = threadIdx.x & 63;
   uint32_t slot = blockIdx.x % kWsSlots;
+  // A claim taken one tile ahead (its atomic issued as a tile starts, read as it
+  // ends) measured 30 us slower on folded c5 (2.656 vs 2.625 ms, 3 reps,
+  // profiles/r06_ws/prefetch/): the atomic sits ahead of the tile's block loads in
+  // the in-order vmcnt, so the first load's wait paid its latency anyway.
   for (;;) {
     const uint32_t cnt = slot < tiles ? (tiles - 1 - slot) / kWsSlots + 1 : 0;
     uint32_t* c = ctr + slot * kWsStride;
@@ -432,6 +436,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch_ws(const uint8_t* __res
       m = v;
     }
     const uint64_t l = live ? len[m] : 0;
+    const uint64_t mo = live ? off[m] : 0;  // issued beside len's load, before the priority's reduction
     // Issue priority by the tile's longest chain. A statically mapped launch
     // dispatches its longest lanes first, and the SIMD's oldest-first issue then
     // runs those chains nearly alone; resident waves are all the same age, so
@@ -450,7 +455,7 @@ __global__ __launch_bounds__(256, 8) void k_digest_batch_ws(const uint8_t* __res
       __builtin_amdgcn_s_setprio(0);
     if (live) {
       const uint64_t o = out_idx ? (uint64_t)out_idx[i] : m;
-      const uint8_t* p = arena + off[m];
+      const uint8_t* p = arena + mo;
       if (check_aligned(p, out + 32 * o, err)) hash_message<MODE>(p, l, out + 32 * o);
       l1 = l + 1;
     }

@@ -645,11 +645,10 @@ __global__ __launch_bounds__(256) void k_fold_keys(FoldArgs a) {
 #pragma unroll 4
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    if (i < a.n) {
-      const uint64_t l = a.len[i];
-      fold_hist_add(hist, l);
-      a.key16[i] = (uint16_t)fold_key(l);
-    }
+    const bool valid = i < a.n;
+    const uint64_t l = valid ? a.len[i] : 0;
+    fold_hist_add_wave(hist, valid, l);  // wave-aggregated (round 6; one LDS atomic per lane serialised)
+    if (valid) a.key16[i] = (uint16_t)fold_key(l);
   }
   __syncthreads();
   fold_hist_flush(a, hist, nkeys);
@@ -822,11 +821,27 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
   }
   __syncthreads();
   const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
+  const unsigned lane = __lane_id();
 #pragma unroll
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
     const uint32_t k = i < a.n ? a.key16[i] : 0xFFFFu;
-    if (k != 0xFFFFu) a.order[atomicAdd(&pos[k], 1u)] = (uint32_t)i;
+    const bool valid = k != 0xFFFFu;
+    // Round 6: the lanes sharing the first valid lane's key (a storm's wave: ~70 %
+    // one key) take their positions with ONE LDS atomic, ranked by lane; 64 atomics
+    // on one LDS word serialise. The rest one each, as before.
+    const uint64_t any = __ballot(valid);
+    if (!any) continue;
+    const uint32_t k0 = __shfl(k, __ffsll((long long)any) - 1);
+    const uint64_t same = __ballot(valid && k == k0);
+    const uint32_t before = (uint32_t)__popcll(same & ((1ull << lane) - 1));
+    uint32_t b0 = 0;
+    if (((same >> lane) & 1) && before == 0) b0 = atomicAdd(&pos[k0], (uint32_t)__popcll(same));
+    b0 = __shfl(b0, __ffsll((long long)same) - 1);
+    if ((same >> lane) & 1)
+      a.order[b0 + before] = (uint32_t)i;
+    else if (valid)
+      a.order[atomicAdd(&pos[k], 1u)] = (uint32_t)i;
   }
   // positions past the last lane (the folded aliases' share) hold kNoLane
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -983,14 +998,17 @@ hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
 // One workgroup per insert tile: its folded messages copy their representative's
 // digest (32 bytes each).
 __global__ __launch_bounds__(256) void k_fold_fill(FoldArgs a, uint8_t* __restrict__ out) {
-  const uint32_t cnt = a.acount[blockIdx.x];
-  const uint64_t* p = a.apairs + (uint64_t)blockIdx.x * kPlanTile;
-  for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
-    const uint64_t v = p[k];
-    const uint4* src = reinterpret_cast<const uint4*>(out + 32 * (v >> 32));
-    uint4* dst = reinterpret_cast<uint4*>(out + 32 * (v & 0xFFFFFFFFull));
-    dst[0] = src[0];
-    dst[1] = src[1];
+  const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
+  for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
+    const uint32_t cnt = a.acount[tile];
+    const uint64_t* p = a.apairs + tile * kPlanTile;
+    for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
+      const uint64_t v = p[k];
+      const uint4* src = reinterpret_cast<const uint4*>(out + 32 * (v >> 32));
+      uint4* dst = reinterpret_cast<uint4*>(out + 32 * (v & 0xFFFFFFFFull));
+      dst[0] = src[0];
+      dst[1] = src[1];
+    }
   }
 }
 
@@ -1019,7 +1037,10 @@ hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_a
 
 hipError_t launch_fold_fill(const FoldArgs& a, uint8_t* out, hipStream_t st) {
   if (a.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_fold_fill, dim3((unsigned)((a.n + kPlanTile - 1) / kPlanTile)), dim3(256), 0, st, a, out);
+  // one workgroup a tile (256 workgroups looping over tiles measured the same:
+  // profiles/r06_ws/prefetch/)
+  const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
+  hipLaunchKernelGGL(k_fold_fill, dim3((unsigned)tiles), dim3(256), 0, st, a, out);
   return hipGetLastError();
 }
 
