@@ -193,7 +193,6 @@ struct FoldArgs {
   // (a long chain there shares a SIMD with same-age waves: kernels.hip); 0: off.
   uint32_t ws_long = 0;
   uint32_t longs_wgs = 0;  // k_fold_longs / k_fold_longs_gate workgroups (0: 4 a CU; A/B MSHA_LONGS_WGS)
-  uint32_t tile_sample = 4;  // k_fold_tilemax sizes every tile_sample-th tile for the first decision
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;

@@ -2991,7 +2991,6 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // pass beside the prefix): off by default (profiles/r06_call4/).
     fa.early_fork = early && env_u64("MSHA_EARLY_FORK", 0) != 0;
     fa.longs_wgs = (uint32_t)env_u64("MSHA_LONGS_WGS", 0);
-    fa.tile_sample = (uint32_t)std::max<uint64_t>(1, env_u64("MSHA_TILE_SAMPLE", 4));
     if (fa.early_fork) {
       HIPCHK(hipEventRecord(d.ev_longs, ps));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));

@@ -359,12 +359,7 @@ __global__ __launch_bounds__(256) void k_fold_tilemax(FoldArgs a) {
 #pragma unroll
   for (uint32_t r = 0; r < kPlanItems; ++r) m = max(m, o[r]);
   part[threadIdx.x] = m;
-  // (else k_fold_longs_gate decides) The early head's first decision from every
-  // tile_sample-th tile's lengths (x tile_sample): tilemax streams off and len, and
-  // the len pass was half its bytes (round 6). A long payload only in unsampled
-  // tiles can make it stand down; the scan's late head then takes that chain
-  // (slower, never wrong).
-  const bool sizes = a.long_blocks && !a.early_fork && blockIdx.x % a.tile_sample == 0;
+  const bool sizes = a.long_blocks && !a.early_fork;  // else k_fold_longs_gate decides
   if (sizes) {
     uint64_t l[kPlanItems];
     load_run(a.len, base, a.n, a.vec, l);
@@ -388,9 +383,9 @@ __global__ __launch_bounds__(256) void k_fold_tilemax(FoldArgs a) {
   }
   if (threadIdx.x == 0) {
     a.tmax[blockIdx.x] = part[0];
-    if (a.long_blocks && !a.early_fork) {
-      a.tsum[2 * blockIdx.x] = sizes ? (s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3]) * a.tile_sample : 0;
-      a.tsum[2 * blockIdx.x + 1] = sizes ? max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3])) : 0;
+    if (sizes) {
+      a.tsum[2 * blockIdx.x] = s_sum[0] + s_sum[1] + s_sum[2] + s_sum[3];
+      a.tsum[2 * blockIdx.x + 1] = max(max(s_max[0], s_max[1]), max(s_max[2], s_max[3]));
     }
   }
 }
@@ -650,10 +645,13 @@ __global__ __launch_bounds__(256) void k_fold_keys(FoldArgs a) {
 #pragma unroll 4
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    const bool valid = i < a.n;
-    const uint64_t l = valid ? a.len[i] : 0;
-    fold_hist_add_wave(hist, valid, l);  // wave-aggregated (round 6; one LDS atomic per lane serialised)
-    if (valid) a.key16[i] = (uint16_t)fold_key(l);
+    // one LDS atomic a message: the wave-aggregated count (k_fold_insert's)
+    // measured slower here, 70.6 -> 84.5 us on c5 (round 6, profiles/r06_plan2/)
+    if (i < a.n) {
+      const uint64_t l = a.len[i];
+      fold_hist_add(hist, l);
+      a.key16[i] = (uint16_t)fold_key(l);
+    }
   }
   __syncthreads();
   fold_hist_flush(a, hist, nkeys);
