@@ -147,6 +147,11 @@ struct FoldArgs {
   uint32_t* acount = nullptr;
   uint64_t* tmax = nullptr;   // (with table) ceil(n / 4096): largest offset before each tile
   uint64_t* tsum = nullptr;   // (early head) 2 per tile: the tile's short messages' blocks, its longest chain
+  // Round 6: (with table, non-null) the insert finds its tile's prefix itself, by a
+  // decoupled look-back over ceil(n / 4096) zeroed status words (plan.hip
+  // tile_lookback) -- no k_fold_tilemax / k_fold_tilescan; then one more zeroed
+  // word: look-backs that gave up waiting (0 expected; see tile_lookback)
+  uint64_t* tstat = nullptr;
   uint32_t* cnt;              // kFoldBuckets zeroed counters (by key) -> bucket starts
   uint64_t* big = nullptr;    // 2 x kFoldBigBuckets zeroed: per power-of-two key, the largest
                               // block count and the block sum (the head's cost model needs the
@@ -193,6 +198,7 @@ struct FoldArgs {
   // (a long chain there shares a SIMD with same-age waves: kernels.hip); 0: off.
   uint32_t ws_long = 0;
   uint32_t longs_wgs = 0;  // k_fold_longs / k_fold_longs_gate workgroups (0: 4 a CU; A/B MSHA_LONGS_WGS)
+  uint32_t gate_wgs = 0;   // k_fold_longs_gate's alone when non-zero (MSHA_GATE_WGS)
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;

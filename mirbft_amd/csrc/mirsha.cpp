@@ -2853,8 +2853,18 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // one zeroed block: info (12 words, padded to 64 bytes), the bucket counters,
     // then FoldArgs::big -- cleared by ONE memset per call
     // (+ the work-stealing lane kernel's tile counters)
-    const uint64_t fold_zero = 64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets +
-                               4 * msha::kWsSlots * msha::kWsStride;
+    const uint64_t fold_zero_fixed = 64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets +
+                                     4 * msha::kWsSlots * msha::kWsStride;
+    // Round 6: a folded call's insert finds its tile prefix by look-back (plan.hip
+    // tile_lookback) over status words zeroed with the rest -- no k_fold_tilemax /
+    // k_fold_tilescan and their two dependent launches. MSHA_FOLD_LOOKBACK=0: the
+    // two-kernel prefix (A/B).
+    const bool lookback = fold && env_u64("MSHA_FOLD_LOOKBACK", 1) != 0;
+    const uint64_t ptiles = (n + 4095) / 4096;
+    static_assert((64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets + 4 * msha::kWsSlots * msha::kWsStride) %
+                      8 == 0,
+                  "the look-back's status words follow 8-byte aligned");
+    const uint64_t fold_zero = fold_zero_fixed + (lookback ? 8 * (ptiles + 1) : 0);
     d.f_cnt.ensure(fold_zero);
     d.f_key.ensure(2 * n);
     d.f_tkeys.ensure(8 * n + 4 * ((n + 4095) / 4096) + 8 * 4096);  // per-tile key lists, then their counts
@@ -2924,6 +2934,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.tkcount = reinterpret_cast<uint32_t*>(fa.tkeys + (n + 4095) / 4096 * 4096);
     fa.big = reinterpret_cast<uint64_t*>(fa.cnt + msha::kFoldBuckets);  // kFoldBuckets is even: 8-byte aligned
     fa.order = d.f_order.as<uint32_t>();
+    fa.tstat = lookback ? reinterpret_cast<uint64_t*>(d.f_cnt.as<uint8_t>() + fold_zero_fixed) : nullptr;
     fa.simds = (uint32_t)d.cus * 4;
     // The head's kernel. Folded, a head is the few distinct long payloads: the
     // two-lane chain (k_digest_chain2, 64 messages per CU, ~10 % fewer cycles a
@@ -2989,8 +3000,12 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // (k_fold_longs_gate over len). The chain then starts ~13 us sooner over 8
     // GPUs with no measurable step change, and one GPU lost ~27 us (the gate's
     // pass beside the prefix): off by default (profiles/r06_call4/).
-    fa.early_fork = early && env_u64("MSHA_EARLY_FORK", 0) != 0;
+    // With the look-back there is no tile prefix to decide in: the gate always
+    // decides, on 64 workgroups (MSHA_GATE_WGS; the 1,024 of the list's grid end in
+    // ~60 us of same-address atomics beside the insert, profiles/r06_call4/).
+    fa.early_fork = early && (lookback || env_u64("MSHA_EARLY_FORK", 0) != 0);
     fa.longs_wgs = (uint32_t)env_u64("MSHA_LONGS_WGS", 0);
+    fa.gate_wgs = (uint32_t)env_u64("MSHA_GATE_WGS", 64);
     if (fa.early_fork) {
       HIPCHK(hipEventRecord(d.ev_longs, ps));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
@@ -3054,10 +3069,18 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       if (early) HIPCHK(hipStreamWaitEvent(st, d.ev_join2, 0));
     }
     if (fold) HIPCHK(msha::launch_fold_fill(fa, d_out, st));
+    if (lookback && env_u64("MSHA_CHECK_LOOKBACK", 0)) {  // tests: no look-back gave up (waits for the call)
+      uint64_t gave_up = 0;
+      HIPCHK(hipStreamSynchronize(st));
+      HIPCHK(hipMemcpy(&gave_up, fa.tstat + ptiles, sizeof gave_up, hipMemcpyDeviceToHost));
+      if (gave_up)
+        throw MshaError(MSHA_ERR_HIP, "planner tile look-back gave up waiting " + std::to_string(gave_up) +
+                                          " time(s) (digests exact, folding reduced)");
+    }
     HIPCHK(hipEventRecord(d.ev_fdone, st));
     d.fdone_recorded = true;
     ctx->stats.planned_device_calls++;
-    if (trace_on()) {  // MSHA_TRACE: the GPU's plan (waits for the call)
+    if (trace_on() || env_u64("MSHA_TRACE_PLAN", 0)) {  // MSHA_TRACE: the GPU's plan (waits for the call)
       uint32_t info[2] = {0, 0};
       HIPCHK(hipStreamSynchronize(st));
       HIPCHK(hipMemcpy(info, fa.info, sizeof info, hipMemcpyDeviceToHost));

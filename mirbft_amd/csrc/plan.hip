@@ -40,6 +40,34 @@
 
 namespace msha {
 
+// Planner stamps: diagnostic build only (-DMSHA_PLAN_STAMPS, tools/plan_stamps.py).
+// Thread 0 of every workgroup of the folded planner's kernels records the 100 MHz
+// wall clock (s_memrealtime) at phase boundaries into a fixed slot (kind, block):
+// 16 words a record, word 15 = HW_ID | XCC_ID << 32. The product build compiles
+// every PLAN_STAMP to nothing.
+enum PlanStampKind : uint32_t { kPsInsert = 0, kPsScatter = 1, kPsScan = 2, kPsFill = 3, kPsGate = 4, kPsLongs = 5 };
+#ifdef MSHA_PLAN_STAMPS
+__device__ uint64_t* g_plan_stamps;
+__device__ uint32_t g_plan_stamp_per;  // records per kind
+__device__ __forceinline__ void plan_stamp(uint32_t kind, uint32_t ph) {
+  if (threadIdx.x != 0 || !g_plan_stamps || blockIdx.x >= g_plan_stamp_per) return;
+  uint64_t* r = g_plan_stamps + ((uint64_t)kind * g_plan_stamp_per + blockIdx.x) * 16;
+  r[ph] = __builtin_amdgcn_s_memrealtime();
+  if (ph == 0)
+    r[15] = (uint64_t)__builtin_amdgcn_s_getreg(4 | (31 << 11)) |
+            ((uint64_t)__builtin_amdgcn_s_getreg(20 | (15 << 11)) << 32);
+}
+__device__ __forceinline__ void plan_stamp_val(uint32_t kind, uint32_t w, uint64_t v) {
+  if (threadIdx.x != 0 || !g_plan_stamps || blockIdx.x >= g_plan_stamp_per) return;
+  g_plan_stamps[((uint64_t)kind * g_plan_stamp_per + blockIdx.x) * 16 + w] = v;
+}
+#define PLAN_STAMP(kind, ph) plan_stamp(kind, ph)
+#define PLAN_STAMP_VAL(kind, w, v) plan_stamp_val(kind, w, v)
+#else
+#define PLAN_STAMP(kind, ph)
+#define PLAN_STAMP_VAL(kind, w, v)
+#endif
+
 __device__ __forceinline__ uint64_t dev_blocks_for(uint64_t len) { return (len >> 6) + ((len & 63) < 56 ? 1 : 2); }
 
 __device__ __forceinline__ uint64_t plan_hash(uint64_t off, uint64_t len) {
@@ -534,6 +562,49 @@ __device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h, 
 // per lane at a 64-byte stride), and the candidates' list is appended and the
 // histogram counted wave-aggregated.
 constexpr uint32_t kLaneMark = 0x80000000u;
+
+// Round 6: the tile prefix inside the insert (FoldArgs::tstat), a decoupled
+// look-back: each tile posts its own largest offset (kTileAgg) as soon as it has
+// it, then wave 0 combines the posts of the tiles before it, 64 a step, back to
+// the nearest tile that has posted its inclusive prefix (kTileIncl), and posts
+// its own. A post is 62 bits of offset (an arena offset past 2^62 bytes is
+// clamped: the threshold then only folds less) and 2 bits of state; 0 = not yet.
+//
+// Waiting is on earlier tiles only, which the dispatcher has placed before this
+// one (in order on each XCD), so it ends; still, a look-back that has waited
+// kLookbackSpins polls gives up and returns the largest threshold, under which no
+// message is fresh and every one claims in the table -- the same digests, less
+// folding -- and counts itself in tstat[tiles] (tests expect 0).
+constexpr uint64_t kTileAgg = 1ull << 62, kTileIncl = 2ull << 62, kTileVal = kTileAgg - 1;
+constexpr uint32_t kLookbackSpins = 1u << 16;
+__device__ __forceinline__ uint64_t tile_lookback(const FoldArgs& a, uint64_t tile) {
+  const unsigned lane = __lane_id();
+  uint64_t acc = 0;
+  uint32_t spins = 0;
+  for (int64_t hi = (int64_t)tile - 1; hi >= 0; hi -= 64) {
+    const int64_t j = hi - (int64_t)lane;  // lane 0 the nearest tile
+    uint64_t v = j >= 0 ? __hip_atomic_load(&a.tstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kTileIncl;
+    while (__ballot(v == 0)) {
+      if (++spins > kLookbackSpins) {
+        if (lane == 0) {
+          const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
+          atomicAdd(reinterpret_cast<unsigned long long*>(&a.tstat[tiles]), 1ull);
+        }
+        return kTileVal;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      if (v == 0) v = __hip_atomic_load(&a.tstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    const uint64_t incl = __ballot((v & ~kTileVal) == kTileIncl);
+    const int stop = incl ? __ffsll((long long)incl) - 1 : 63;  // lanes 0..stop count
+    uint64_t x = (int)lane <= stop ? (v & kTileVal) : 0ull;
+    for (uint32_t d = 32; d > 0; d >>= 1) x = max(x, (uint64_t)__shfl_xor(x, d));
+    acc = max(acc, x);
+    if (incl) break;
+  }
+  return acc;
+}
+
 __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   __shared__ uint64_t part[256];
   __shared__ FoldHist hist;
@@ -542,6 +613,8 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
   __shared__ uint32_t trep[kPlanTile];
   __shared__ uint16_t cand[kPlanTile];   // candidates' positions in the tile
   __shared__ uint32_t ncand, nalias, nkeys;
+  __shared__ uint64_t s_before;  // (tstat) the largest offset of the tiles before this one
+  PLAN_STAMP(kPsInsert, 0);
   fold_hist_clear(hist);
   if (threadIdx.x == 0) ncand = nalias = nkeys = 0;
   const uint64_t tile0 = (uint64_t)blockIdx.x * kPlanTile;
@@ -554,6 +627,7 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
 #pragma unroll
   for (uint32_t r = 0; r < kPlanItems; ++r) m = max(m, o[r]);
   part[threadIdx.x] = m;
+  PLAN_STAMP(kPsInsert, 1);
   __syncthreads();
   for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive prefix max over the tile's threads
     const uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0ull;
@@ -561,8 +635,31 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     part[threadIdx.x] = max(part[threadIdx.x], v);
     __syncthreads();
   }
+  PLAN_STAMP(kPsInsert, 2);
+  uint64_t before;
+  if (a.tstat) {
+    if (threadIdx.x < 64) {
+      const uint64_t own = min(part[255], kTileVal);
+      if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) __hip_atomic_store(&a.tstat[0], kTileIncl | own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        if (threadIdx.x == 0) __hip_atomic_store(&a.tstat[blockIdx.x], kTileAgg | own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const uint64_t b = tile_lookback(a, blockIdx.x);
+        if (threadIdx.x == 0) {
+          s_before = b;
+          __hip_atomic_store(&a.tstat[blockIdx.x], kTileIncl | max(b, own), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      if (blockIdx.x == 0 && threadIdx.x == 0) s_before = 0;
+    }
+    __syncthreads();
+    before = s_before;
+  } else {
+    before = a.tmax[blockIdx.x];
+  }
+  PLAN_STAMP(kPsInsert, 3);
   const bool first_ever = blockIdx.x == 0 && threadIdx.x == 0;
-  uint64_t run = max(a.tmax[blockIdx.x], threadIdx.x ? part[threadIdx.x - 1] : 0ull);
+  uint64_t run = max(before, threadIdx.x ? part[threadIdx.x - 1] : 0ull);
   const unsigned lane = __lane_id();
   // Candidates are few (c5: 5 %) but spread over every wave: claiming them in
   // place would run each wave's claim loop (a load -> CAS -> compare chain of
@@ -590,6 +687,8 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     run = max(run, o[r]);
   }
   __syncthreads();
+  PLAN_STAMP(kPsInsert, 4);
+  PLAN_STAMP_VAL(kPsInsert, 8, ncand);
   for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
     const uint32_t li = cand[c];
     const uint64_t i = tile0 + li;
@@ -599,6 +698,7 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     if (rp == (uint32_t)i) fold_hist_add(hist, ln);
   }
   __syncthreads();
+  PLAN_STAMP(kPsInsert, 5);
   // lane keys out, consecutive messages per wave instruction; the folded messages
   // as (rep, i) pairs into the tile's segment of apairs, so the fill reads only
   // them (c5: 5 % of the messages) instead of a representative per message
@@ -620,8 +720,11 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
       if (folded) a.apairs[tile0 + at + (uint32_t)__popcll(fm & ((1ull << lane) - 1))] = ((uint64_t)v << 32) | (uint32_t)i;
     }
   }
+  PLAN_STAMP(kPsInsert, 6);
   fold_hist_flush(a, hist, nkeys);  // (its barrier also completes nalias)
   if (threadIdx.x == 0) a.acount[blockIdx.x] = nalias;
+  PLAN_STAMP(kPsInsert, 7);
+  PLAN_STAMP_VAL(kPsInsert, 9, nkeys);
 }
 
 // The fold planner's keys are few (kFoldBuckets), so a tile counts them in a
@@ -703,6 +806,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   __shared__ uint64_t blk[1024];
   __shared__ uint64_t best[1024];
   __shared__ uint32_t s_long;  // lanes of >= long_blocks blocks
+  PLAN_STAMP(kPsScan, 0);
   const uint32_t t = threadIdx.x;
   if (t == 0) s_long = 0;
   constexpr uint32_t per = (kFoldBuckets + 1023) / 1024;
@@ -806,6 +910,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     a.info[0] = lanes;
     a.info[1] = early ? early : late;
     a.info[5] = early ? 0u : late;
+    PLAN_STAMP(kPsScan, 1);
   }
 }
 
@@ -816,6 +921,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
 // keys of a storm.
 __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
   __shared__ uint32_t pos[kFoldBuckets];  // next position of each key the tile holds
+  PLAN_STAMP(kPsScatter, 0);
   const uint32_t nk = a.tkcount[blockIdx.x];
   const uint64_t* tl = a.tkeys + (uint64_t)blockIdx.x * kPlanTile;
   for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) {
@@ -823,6 +929,7 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
     pos[v >> 32] = a.cnt[v >> 32] + (uint32_t)v;  // bucket start (k_fold_scan) + the tile's offset
   }
   __syncthreads();
+  PLAN_STAMP(kPsScatter, 1);
   const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
   const unsigned lane = __lane_id();
 #pragma unroll
@@ -846,10 +953,12 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
     else if (valid)
       a.order[atomicAdd(&pos[k], 1u)] = (uint32_t)i;
   }
+  PLAN_STAMP(kPsScatter, 2);
   // positions past the last lane (the folded aliases' share) hold kNoLane
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t q = a.info[0] + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < a.n; q += stride)
     a.order[q] = kNoLane;
+  PLAN_STAMP(kPsScatter, 3);
 }
 
 // The early head's list: every message of >= long_blocks blocks claims its
@@ -945,6 +1054,7 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
 __global__ __launch_bounds__(256) void k_fold_longs_gate(FoldArgs a) {
   __shared__ unsigned long long s_sum, s_max;
   __shared__ bool last;
+  PLAN_STAMP(kPsGate, 0);
   if (threadIdx.x == 0) s_sum = s_max = 0;
   __syncthreads();
   uint64_t sum = 0, mx = 0;
@@ -985,15 +1095,18 @@ __global__ __launch_bounds__(256) void k_fold_longs_gate(FoldArgs a) {
     const uint64_t t_head = sm * a.early_cycles;
     a.info[6] = sm >= a.long_blocks && t_body < t_head ? 1u : 0u;
   }
+  PLAN_STAMP(kPsGate, 1);
 }
 
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
   if (a.n == 0 || !a.long_blocks) return hipSuccess;
   // a.longs_wgs (A/B): fewer workgroups, fewer of the same-address atomics that end
   // each one (each costs ~20 ns serialised: profiles/r06_call4/)
+  const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
   const uint64_t cap = a.longs_wgs ? a.longs_wgs : (uint64_t)cus * 4;
-  const unsigned grid = (unsigned)std::min<uint64_t>((a.n + kPlanTile - 1) / kPlanTile, cap);
-  if (a.early_fork) hipLaunchKernelGGL(k_fold_longs_gate, dim3(grid), dim3(256), 0, st, a);
+  const unsigned grid = (unsigned)std::min<uint64_t>(tiles, cap);
+  const unsigned ggrid = a.gate_wgs ? (unsigned)std::min<uint64_t>(tiles, a.gate_wgs) : grid;
+  if (a.early_fork) hipLaunchKernelGGL(k_fold_longs_gate, dim3(ggrid), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_longs, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
 }
@@ -1001,6 +1114,7 @@ hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
 // One workgroup per insert tile: its folded messages copy their representative's
 // digest (32 bytes each).
 __global__ __launch_bounds__(256) void k_fold_fill(FoldArgs a, uint8_t* __restrict__ out) {
+  PLAN_STAMP(kPsFill, 0);
   const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
   for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
     const uint32_t cnt = a.acount[tile];
@@ -1013,10 +1127,11 @@ __global__ __launch_bounds__(256) void k_fold_fill(FoldArgs a, uint8_t* __restri
       dst[1] = src[1];
     }
   }
+  PLAN_STAMP(kPsFill, 1);
 }
 
 hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st) {
-  if (a.n == 0 || !a.table) return hipSuccess;
+  if (a.n == 0 || !a.table || a.tstat) return hipSuccess;  // (tstat: the insert looks back itself)
   const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
   hipLaunchKernelGGL(k_fold_tilemax, dim3(ptiles), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_tilescan, dim3(1), dim3(1024), 0, st, a, (uint64_t)ptiles);
@@ -1048,3 +1163,14 @@ hipError_t launch_fold_fill(const FoldArgs& a, uint8_t* out, hipStream_t st) {
 }
 
 }  // namespace msha
+
+#ifdef MSHA_PLAN_STAMPS
+// Diagnostic build only: points the planner stamps at `buf` (device memory, 6 x per
+// records of 16 words; the caller zeroes it before the call it wants). NULL: off.
+extern "C" int msha_diag_plan_stamps(void* buf, uint32_t per) {
+  uint64_t* b = static_cast<uint64_t*>(buf);
+  if (hipMemcpyToSymbol(HIP_SYMBOL(msha::g_plan_stamps), &b, sizeof b) != hipSuccess) return 3;
+  if (hipMemcpyToSymbol(HIP_SYMBOL(msha::g_plan_stamp_per), &per, sizeof per) != hipSuccess) return 3;
+  return hipDeviceSynchronize() == hipSuccess ? 0 : 3;
+}
+#endif

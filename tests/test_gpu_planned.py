@@ -17,6 +17,14 @@ from oracle import oracle
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _lookback_checked(monkeypatch):
+    """Every planned call here fails if a folded insert's tile look-back gave up
+    waiting for an earlier tile (plan.hip tile_lookback: the digests would still be
+    exact, with less folding, so only this check can see it)."""
+    monkeypatch.setenv("MSHA_CHECK_LOOKBACK", "1")
+
+
 def _dev(w):
     import torch
     dev = torch.device("cuda:0")
@@ -412,12 +420,14 @@ def test_early_head_batches(engine, monkeypatch, case):
     _assert_head_kernels(before, engine.stats(), True)
 
 
-def test_tile_backrefs(engine):
+@pytest.mark.parametrize("lookback", ["1", "0"])
+def test_tile_backrefs(engine, monkeypatch, lookback):
     """Candidates-first folding across tiles: a message skips the alias table only
-    when its offset is above every earlier message's, which the tile prefix
-    (k_fold_tilemax, k_fold_tilescan) carries from tile to tile. Here every tile
-    of 4,096 messages names payloads of the tile before it again (10 % of its
-    messages). Every digest exact."""
+    when its offset is above every earlier message's, which the tile prefix carries
+    from tile to tile -- the insert's own look-back (default) or k_fold_tilemax and
+    k_fold_tilescan (MSHA_FOLD_LOOKBACK=0). Here every tile of 4,096 messages names
+    payloads of the tile before it again (10 % of its messages). Every digest exact."""
+    monkeypatch.setenv("MSHA_FOLD_LOOKBACK", lookback)
     rng = np.random.default_rng(0x1B)
     n = 300_000
     ln = rng.integers(0, 700, n).astype(np.uint64)
@@ -427,6 +437,27 @@ def test_tile_backrefs(engine):
     off[back], ln[back] = off[src[back]], ln[src[back]]
     w = W.Workload("tile-backrefs", arena, off, ln)
     assert np.array_equal(_run(engine, w, True), _expect(w))
+
+
+@pytest.mark.parametrize("world", [1, 8])
+def test_lookback_folds_as_the_prefix(engine, monkeypatch, capfd, world):
+    """The insert's tile look-back hands every tile the same threshold as the
+    two-kernel prefix: a c5 slice folded both ways has the same number of lanes
+    (MSHA_TRACE_PLAN prints the GPU's plan; lanes = fresh messages + one claimant per
+    repeated payload, independent of which message wins a claim), digests exact."""
+    w = W.c5_storm(n=(1 << 23) // world)
+    exp = _expect(w)
+    monkeypatch.setenv("MSHA_TRACE_PLAN", "1")
+    lanes = {}
+    for lb in ("1", "0"):
+        monkeypatch.setenv("MSHA_FOLD_LOOKBACK", lb)
+        capfd.readouterr()
+        assert np.array_equal(_run(engine, w, True), exp)
+        err = capfd.readouterr().err
+        lines = [l for l in err.splitlines() if "planned device call" in l]
+        assert len(lines) == 1, err
+        lanes[lb] = int(lines[0].split(",")[1].split()[0])
+    assert lanes["1"] == lanes["0"] and 0 < lanes["1"] < w.n, lanes
 
 
 @pytest.mark.parametrize("world", [2, 8])
