@@ -172,8 +172,10 @@ struct FoldArgs {
                               // [6] the first decision (0: no early head), by k_fold_tilescan,
                               // or with early_fork by k_fold_longs_gate ([7]: its workgroups
                               // done, [12..15] two u64: the short blocks and longest chain),
-                              // [8..11] two u64: the batch's blocks and longest chain
-                              // (all 16 words zeroed by the caller)
+                              // [8..11] two u64: the batch's blocks and longest chain,
+                              // [16] lanes of >= long_blocks blocks, [17] the scan's cut (the
+                              // scatter resolves [1] and [5] from them and [4])
+                              // (all 32 words zeroed by the caller)
   // The early head (folding only; long_blocks 0: off): k_fold_tilescan sizes the
   // batch (info[6]: 0 when the short messages alone outlast the longest chain);
   // unless it stood down there, k_fold_longs claims every message of >=
@@ -198,7 +200,7 @@ struct FoldArgs {
   // (a long chain there shares a SIMD with same-age waves: kernels.hip); 0: off.
   uint32_t ws_long = 0;
   uint32_t longs_wgs = 0;  // k_fold_longs / k_fold_longs_gate workgroups (0: 4 a CU; A/B MSHA_LONGS_WGS)
-  uint32_t gate_wgs = 0;   // k_fold_longs_gate's alone when non-zero (MSHA_GATE_WGS)
+  uint32_t gate_wgs = 0;   // k_fold_longs_gate's workgroups (0: 64; MSHA_GATE_WGS)
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;
@@ -221,15 +223,16 @@ struct FoldArgs {
   uint32_t tiebreak = 1;         // head-bound ties go to the cut with the most lane-kernel room (A/B: 0)
   // test build only (-DMSHA_FOLD_RACE_TEST, MSHA_FOLD_LONGS_SKIP_ODD=1): k_fold_longs
   // leaves every long payload whose table hash is odd unlisted, a state the product
-  // kernels cannot reach, to exercise k_fold_scan's defensive check
+  // kernels cannot reach, to exercise the scan/scatter defensive check
   uint32_t race_test = 0;
 };
 // Folding only: the tile maxima and their prefix (k_fold_tilemax, k_fold_tilescan),
 // with the early head's list and decision when long_blocks is set; then
 // launch_fold_plan: the insert (or, unfolded, the counts), scan and scatter.
 hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st);
-// scan_after (may be null): an event k_fold_scan waits for (the early head's list).
-hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_after = nullptr);
+// scatter_after (may be null): an event k_fold_scatter waits for (the early head's
+// list: the scatter resolves the heads against it).
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scatter_after = nullptr);
 // The early head's list (FoldArgs::longs): on a stream of its own, after the
 // prefix, beside the alias insert (both claim through the same table).
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st);

@@ -2850,10 +2850,10 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     const bool head = !all_coop && ctx->kernel_policy != MSHA_KERNEL_LANE && env_u64("MSHA_PLAN_HEAD", 1) != 0;
     uint64_t cap = 1024;
     while (cap < 2 * n) cap <<= 1;
-    // one zeroed block: info (12 words, padded to 64 bytes), the bucket counters,
+    // one zeroed block: info (32 words, 128 bytes), the bucket counters,
     // then FoldArgs::big -- cleared by ONE memset per call
     // (+ the work-stealing lane kernel's tile counters)
-    const uint64_t fold_zero_fixed = 64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets +
+    const uint64_t fold_zero_fixed = 128 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets +
                                      4 * msha::kWsSlots * msha::kWsStride;
     // Round 6: a folded call's insert finds its tile prefix by look-back (plan.hip
     // tile_lookback) over status words zeroed with the rest -- no k_fold_tilemax /
@@ -2861,10 +2861,11 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // two-kernel prefix (A/B).
     const bool lookback = fold && env_u64("MSHA_FOLD_LOOKBACK", 1) != 0;
     const uint64_t ptiles = (n + 4095) / 4096;
-    static_assert((64 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets + 4 * msha::kWsSlots * msha::kWsStride) %
+    static_assert((128 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets + 4 * msha::kWsSlots * msha::kWsStride) %
                       8 == 0,
                   "the look-back's status words follow 8-byte aligned");
-    const uint64_t fold_zero = fold_zero_fixed + (lookback ? 8 * (ptiles + 1) : 0);
+    // (a multiple of 64 bytes: an unaligned tail made hipMemsetAsync a second fill kernel)
+    const uint64_t fold_zero = (fold_zero_fixed + (lookback ? 8 * (ptiles + 1) : 0) + 63) / 64 * 64;
     d.f_cnt.ensure(fold_zero);
     d.f_key.ensure(2 * n);
     d.f_tkeys.ensure(8 * n + 4 * ((n + 4095) / 4096) + 8 * 4096);  // per-tile key lists, then their counts
@@ -2928,7 +2929,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.tmax = fold ? d.f_tmax.as<uint64_t>() : nullptr;
     fa.tsum = fold ? fa.tmax + (n + 4095) / 4096 : nullptr;
     fa.info = d.f_cnt.as<uint32_t>();
-    fa.cnt = fa.info + 16;
+    fa.cnt = fa.info + 32;
     fa.key16 = d.f_key.as<uint16_t>();
     fa.tkeys = d.f_tkeys.as<uint64_t>();
     fa.tkcount = reinterpret_cast<uint32_t*>(fa.tkeys + (n + 4095) / 4096 * 4096);
@@ -3001,11 +3002,10 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // GPUs with no measurable step change, and one GPU lost ~27 us (the gate's
     // pass beside the prefix): off by default (profiles/r06_call4/).
     // With the look-back there is no tile prefix to decide in: the gate always
-    // decides, on 64 workgroups (MSHA_GATE_WGS; the 1,024 of the list's grid end in
-    // ~60 us of same-address atomics beside the insert, profiles/r06_call4/).
+    // decides (64 workgroups; MSHA_GATE_WGS).
     fa.early_fork = early && (lookback || env_u64("MSHA_EARLY_FORK", 0) != 0);
     fa.longs_wgs = (uint32_t)env_u64("MSHA_LONGS_WGS", 0);
-    fa.gate_wgs = (uint32_t)env_u64("MSHA_GATE_WGS", 64);
+    fa.gate_wgs = (uint32_t)env_u64("MSHA_GATE_WGS", 0);
     if (fa.early_fork) {
       HIPCHK(hipEventRecord(d.ev_longs, ps));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));

@@ -534,6 +534,22 @@ __device__ __forceinline__ void fold_hist_add_wave(FoldHist& h, bool valid, uint
   }
   if (valid) fold_hist_big(h, k, blocks);
 }
+// The same by key, for message i (its length is read again only for the rare
+// power-of-two classes, whose block counts the head's cost model needs exactly).
+__device__ __forceinline__ void fold_hist_add_wave_key(const FoldArgs& a, FoldHist& h, bool valid, uint32_t k,
+                                                       uint64_t i) {
+  const uint64_t any = __ballot(valid);
+  if (!any) return;
+  const uint32_t k0 = __shfl(k, __ffsll((long long)any) - 1);
+  const uint64_t same = __ballot(valid && k == k0);
+  const unsigned lane = __lane_id();
+  if ((same >> lane) & 1) {
+    if ((same & ((1ull << lane) - 1)) == 0) atomicAdd(&h.n[k0], (uint32_t)__popcll(same));
+  } else if (valid) {
+    atomicAdd(&h.n[k], 1u);
+  }
+  if (valid && k < kFoldBigBuckets) fold_hist_big(h, k, dev_blocks_for(a.len[i]));
+}
 // Each key present in the tile: one global atomic, whose return is the tile's
 // offset in the key's bucket, kept in the tile's key list (FoldArgs::tkeys) for
 // the scatter. nk: an LDS counter the caller zeroed before a barrier; every
@@ -557,11 +573,10 @@ __device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h, 
 // does without folding): a fresh message is its own lane, a candidate is one
 // when its claim returns itself -- so the lanes' metadata is read once.
 // Round 5: each thread's 16 consecutive (off, len) load as 16-byte vectors
-// (load_run), the tile's representatives gather in LDS and go out as 4-byte
-// words of consecutive messages per wave instruction (whole lines, not 4 bytes
-// per lane at a 64-byte stride), and the candidates' list is appended and the
-// histogram counted wave-aggregated.
-constexpr uint32_t kLaneMark = 0x80000000u;
+// (load_run), the tile's keys gather in LDS and go out as words of consecutive
+// messages per wave instruction (whole lines, not 2 bytes per lane at a 32-byte
+// stride), and the candidates' list is appended and the histogram counted
+// wave-aggregated.
 
 // Round 6: the tile prefix inside the insert (FoldArgs::tstat), a decoupled
 // look-back: each tile posts its own largest offset (kTileAgg) as soon as it has
@@ -605,66 +620,63 @@ __device__ __forceinline__ uint64_t tile_lookback(const FoldArgs& a, uint64_t ti
   return acc;
 }
 
-__global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
-  __shared__ uint64_t part[256];
+// trep's index of tile position p: a pad word after every 16, so the per-thread
+// runs (thread t writes positions 16 t + r) hit 32 different banks, not 2
+__device__ __forceinline__ uint32_t trep_at(uint32_t p) { return p + (p >> 4); }
+
+__global__ __launch_bounds__(256, 4) void k_fold_insert(FoldArgs a) {
+  __shared__ uint64_t wmax[4];
   __shared__ FoldHist hist;
-  // the tile's representatives by position, a lane's as kLaneMark | its key
-  // (planned batches hold < 2^31 messages, mirsha.cpp: no index has that bit)
-  __shared__ uint32_t trep[kPlanTile];
+  // the tile's key16 by position (trep_at): a lane's key, 0xFFFF for a folded
+  // message (whose (rep, i) pair the claim writes). Round 6: 16 bits, not a 32-bit
+  // representative a message -- 4 workgroups a CU in LDS instead of 3.
+  __shared__ uint16_t trep[kPlanTile + kPlanTile / 16];
   __shared__ uint16_t cand[kPlanTile];   // candidates' positions in the tile
   __shared__ uint32_t ncand, nalias, nkeys;
-  __shared__ uint64_t s_before;  // (tstat) the largest offset of the tiles before this one
+  __shared__ uint64_t s_before;  // the largest offset of the tiles before this one
   PLAN_STAMP(kPsInsert, 0);
   fold_hist_clear(hist);
   if (threadIdx.x == 0) ncand = nalias = nkeys = 0;
   const uint64_t tile0 = (uint64_t)blockIdx.x * kPlanTile;
   const uint32_t lb = threadIdx.x * kPlanItems;
   const uint64_t base = tile0 + lb;
+  const unsigned lane = __lane_id(), wave = threadIdx.x >> 6;
   uint64_t o[kPlanItems], l[kPlanItems];
   load_run(a.off, base, a.n, a.vec, o);
   load_run(a.len, base, a.n, a.vec, l);
   uint64_t m = 0;
 #pragma unroll
   for (uint32_t r = 0; r < kPlanItems; ++r) m = max(m, o[r]);
-  part[threadIdx.x] = m;
   PLAN_STAMP(kPsInsert, 1);
+  // in-tile prefix max: inclusive over the wave by shuffles, then the waves before
+  uint64_t incl = m;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t v = (uint64_t)__shfl_up((unsigned long long)incl, d);
+    if (lane >= d) incl = max(incl, v);
+  }
+  if (lane == 63) wmax[wave] = incl;
   __syncthreads();
-  for (uint32_t d = 1; d < 256; d <<= 1) {  // inclusive prefix max over the tile's threads
-    const uint64_t v = threadIdx.x >= d ? part[threadIdx.x - d] : 0ull;
-    __syncthreads();
-    part[threadIdx.x] = max(part[threadIdx.x], v);
-    __syncthreads();
+  uint64_t run = (uint64_t)__shfl_up((unsigned long long)incl, 1);
+  if (lane == 0) run = 0;
+  for (uint32_t w = 0; w < wave; ++w) run = max(run, wmax[w]);  // max offset before this thread's run
+  // Round 6: the tile's own largest offset is posted before anything else, and the
+  // look-back (wave 0, after its share of the first pass) then overlaps the other
+  // waves' first pass; the tiles before this one are applied in a second pass.
+  if (a.tstat && threadIdx.x == 0) {
+    const uint64_t own = min(max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])), kTileVal);
+    __hip_atomic_store(&a.tstat[blockIdx.x], (blockIdx.x ? kTileAgg : kTileIncl) | own, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
   PLAN_STAMP(kPsInsert, 2);
-  uint64_t before;
-  if (a.tstat) {
-    if (threadIdx.x < 64) {
-      const uint64_t own = min(part[255], kTileVal);
-      if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) __hip_atomic_store(&a.tstat[0], kTileIncl | own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      } else {
-        if (threadIdx.x == 0) __hip_atomic_store(&a.tstat[blockIdx.x], kTileAgg | own, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const uint64_t b = tile_lookback(a, blockIdx.x);
-        if (threadIdx.x == 0) {
-          s_before = b;
-          __hip_atomic_store(&a.tstat[blockIdx.x], kTileIncl | max(b, own), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      }
-      if (blockIdx.x == 0 && threadIdx.x == 0) s_before = 0;
-    }
-    __syncthreads();
-    before = s_before;
-  } else {
-    before = a.tmax[blockIdx.x];
-  }
-  PLAN_STAMP(kPsInsert, 3);
   const bool first_ever = blockIdx.x == 0 && threadIdx.x == 0;
-  uint64_t run = max(before, threadIdx.x ? part[threadIdx.x - 1] : 0ull);
-  const unsigned lane = __lane_id();
   // Candidates are few (c5: 5 %) but spread over every wave: claiming them in
   // place would run each wave's claim loop (a load -> CAS -> compare chain of
   // memory round trips) once per item row. They go to an LDS list instead and
   // the workgroup's threads claim them side by side.
+  // First pass, against the tile's own earlier messages only: a message above them
+  // all is fresh so far (bit r of `local`), the rest are candidates.
+  uint32_t local = 0;
+  uint32_t kk[kPlanItems / 2] = {};
 #pragma unroll
   for (uint32_t r = 0; r < kPlanItems; ++r) {
     const uint64_t i = base + r;
@@ -674,8 +686,14 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     const bool lng = valid && a.long_blocks && dev_blocks_for(l[r]) >= a.long_blocks;
     const bool fresh = valid && !lng && (o[r] > run || (first_ever && r == 0));
     const bool is_cand = valid && !fresh;
-    if (fresh) trep[lb + r] = kLaneMark | fold_key(l[r]);
-    fold_hist_add_wave(hist, fresh, l[r]);
+    const uint32_t k = fold_key(l[r]);
+    // the keys, two a register: the lengths are dead after this pass (the insert
+    // then fits 128 VGPRs, 4 waves a SIMD, without spilling)
+    kk[r / 2] |= (r & 1) ? k << 16 : k;
+    if (fresh) {
+      trep[trep_at(lb + r)] = (uint16_t)k;
+      local |= 1u << r;
+    }
     const uint64_t cm = __ballot(is_cand);
     if (cm) {
       uint32_t at = 0;
@@ -686,39 +704,79 @@ __global__ __launch_bounds__(256) void k_fold_insert(FoldArgs a) {
     }
     run = max(run, o[r]);
   }
+  if (wave == 0) {
+    uint64_t b = 0;
+    if (!a.tstat) {
+      b = a.tmax[blockIdx.x];
+    } else if (blockIdx.x) {
+      b = tile_lookback(a, blockIdx.x);
+      if (threadIdx.x == 0) {
+        const uint64_t own = min(max(max(wmax[0], wmax[1]), max(wmax[2], wmax[3])), kTileVal);
+        __hip_atomic_store(&a.tstat[blockIdx.x], kTileIncl | max(b, own), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    if (threadIdx.x == 0) s_before = b;
+  }
+  __syncthreads();
+  PLAN_STAMP(kPsInsert, 3);
+  // Second pass: a message fresh so far stays fresh when it is also above every
+  // offset of the tiles before (tile 0: none); otherwise it joins the candidates
+  // (c5: none -- the packed payloads' offsets rise). The lanes are counted here.
+  const uint64_t before = s_before;
+  const bool check = blockIdx.x != 0;
+#pragma unroll
+  for (uint32_t r = 0; r < kPlanItems; ++r) {
+    const bool was = (local >> r) & 1;
+    const bool fresh = was && (!check || o[r] > before);
+    fold_hist_add_wave_key(a, hist, fresh, (kk[r / 2] >> ((r & 1) * 16)) & 0xFFFFu, base + r);
+    const bool demoted = was && !fresh;
+    const uint64_t cm = __ballot(demoted);
+    if (cm) {
+      uint32_t at = 0;
+      const int leader = __ffsll((long long)cm) - 1;
+      if ((int)lane == leader) at = atomicAdd(&ncand, (uint32_t)__popcll(cm));
+      at = __shfl(at, leader);
+      if (demoted) cand[at + (uint32_t)__popcll(cm & ((1ull << lane) - 1))] = (uint16_t)(lb + r);
+    }
+  }
   __syncthreads();
   PLAN_STAMP(kPsInsert, 4);
   PLAN_STAMP_VAL(kPsInsert, 8, ncand);
-  for (uint32_t c = threadIdx.x; c < ncand; c += blockDim.x) {
-    const uint32_t li = cand[c];
-    const uint64_t i = tile0 + li;
-    const uint64_t ln = a.len[i];
-    const uint32_t rp = fold_claim(a, i, a.off[i], ln);
-    trep[li] = rp == (uint32_t)i ? kLaneMark | fold_key(ln) : rp;
-    if (rp == (uint32_t)i) fold_hist_add(hist, ln);
-  }
-  __syncthreads();
-  PLAN_STAMP(kPsInsert, 5);
-  // lane keys out, consecutive messages per wave instruction; the folded messages
-  // as (rep, i) pairs into the tile's segment of apairs, so the fill reads only
-  // them (c5: 5 % of the messages) instead of a representative per message
-#pragma unroll 4
-  for (uint32_t r = 0; r < kPlanItems; ++r) {
-    const uint32_t li = r * 256 + threadIdx.x;
-    const uint64_t i = tile0 + li;
-    const bool valid = i < a.n;
-    const uint32_t v = valid ? trep[li] : 0u;
-    const bool lane_i = v & kLaneMark;
-    if (valid) a.key16[i] = lane_i ? (uint16_t)(v & 0xFFFFu) : (uint16_t)0xFFFFu;
-    const bool folded = valid && !lane_i;
+  // the claims, side by side; a folded message's (rep, i) pair goes straight into
+  // the tile's segment of apairs, so the fill reads only them (c5: 5 % of the
+  // messages) instead of a representative per message
+  const uint32_t nc = ncand;
+  for (uint32_t c0 = 0; c0 < nc; c0 += blockDim.x) {
+    const uint32_t c = c0 + threadIdx.x;
+    uint32_t li = 0, rp = 0;
+    uint64_t i = 0;
+    if (c < nc) {
+      li = cand[c];
+      i = tile0 + li;
+      const uint64_t ln = a.len[i];
+      rp = fold_claim(a, i, a.off[i], ln);
+      if (rp == (uint32_t)i) fold_hist_add(hist, ln);
+      trep[trep_at(li)] = rp == (uint32_t)i ? (uint16_t)fold_key(ln) : (uint16_t)0xFFFFu;
+    }
+    const bool folded = c < nc && rp != (uint32_t)i;
     const uint64_t fm = __ballot(folded);
     if (fm) {
       uint32_t at = 0;
       const int leader = __ffsll((long long)fm) - 1;
       if ((int)lane == leader) at = atomicAdd(&nalias, (uint32_t)__popcll(fm));
       at = __shfl(at, leader);
-      if (folded) a.apairs[tile0 + at + (uint32_t)__popcll(fm & ((1ull << lane) - 1))] = ((uint64_t)v << 32) | (uint32_t)i;
+      if (folded) a.apairs[tile0 + at + (uint32_t)__popcll(fm & ((1ull << lane) - 1))] = ((uint64_t)rp << 32) | (uint32_t)i;
     }
+  }
+  __syncthreads();
+  PLAN_STAMP(kPsInsert, 5);
+  // key16 out, consecutive messages per wave instruction
+#pragma unroll 4
+  for (uint32_t r = 0; r < kPlanItems; ++r) {
+    const uint32_t li = r * 256 + threadIdx.x;
+    const uint64_t i = tile0 + li;
+    if (i < a.n) a.key16[i] = trep[trep_at(li)];
   }
   PLAN_STAMP(kPsInsert, 6);
   fold_hist_flush(a, hist, nkeys);  // (its barrier also completes nalias)
@@ -788,10 +846,15 @@ __device__ __forceinline__ uint64_t key_sum_blocks(const FoldArgs& a, uint32_t k
 // head, large = none).
 __device__ __forceinline__ uint64_t head_cost(const FoldArgs& a, uint64_t h, uint64_t bh, uint64_t btot,
                                               uint64_t max_blocks, uint64_t next_blocks) {
-  const uint64_t cus = a.simds / 4, hcus = (h + a.head_per_wg - 1) / a.head_per_wg;
-  if (h > a.head_cap || hcus >= cus) return ~0ull;
+  // (k_fold_scan evaluates this for every non-empty bucket on one CU: the 64-bit
+  // divisions it used to make were most of the scan's time. h <= head_cap fits 32
+  // bits; the body's quotient is exact in double below 2^53, far above any batch.)
+  if (h > a.head_cap) return ~0ull;
+  const uint64_t cus = a.simds / 4, hcus = ((uint32_t)h + a.head_per_wg - 1u) / a.head_per_wg;
+  if (hcus >= cus) return ~0ull;
   const uint64_t t_head = h ? max_blocks * a.coop_cycles / 100 * a.head_pct : 0;
-  const uint64_t t_body = (btot - bh) * a.wave_block_cycles / (64ull * 4 * (cus - hcus));
+  const uint64_t t_body =
+      (uint64_t)((double)((btot - bh) * a.wave_block_cycles) / (double)(64ull * 4 * (cus - hcus)));
   const uint64_t t_lanes = max(t_body, next_blocks * a.lane_cycles);
   // work-stealing lane kernel: a cut that leaves a long chain on it loses to any
   // that does not (FoldArgs::ws_long)
@@ -801,63 +864,67 @@ __device__ __forceinline__ uint64_t head_cost(const FoldArgs& a, uint64_t h, uin
 
 constexpr uint64_t kCostMax = (uint64_t(1) << 40) - 1;
 
+// Round 6: each thread's six buckets are read ONCE into registers, and the scans
+// and reductions run over the wave by shuffles, then over the 16 waves' totals in
+// LDS -- 3 barriers instead of ~40, and no loop of dependent bucket loads (the
+// longest-chain search read up to six counters one after another): 14 -> ~3 us.
 __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
-  __shared__ uint32_t part[1024];
-  __shared__ uint64_t blk[1024];
-  __shared__ uint64_t best[1024];
+  __shared__ uint32_t w_cnt[16], w_min[16], w_h[16];
+  __shared__ uint64_t w_blk[16], w_key[16];
   __shared__ uint32_t s_long;  // lanes of >= long_blocks blocks
   PLAN_STAMP(kPsScan, 0);
-  const uint32_t t = threadIdx.x;
+  const uint32_t t = threadIdx.x, lane = __lane_id(), wave = t >> 6;
   if (t == 0) s_long = 0;
   constexpr uint32_t per = (kFoldBuckets + 1023) / 1024;
-  const uint32_t b0 = min(t * per, kFoldBuckets), b1 = min(b0 + per, kFoldBuckets);
-  uint32_t s = 0;
+  const uint32_t b0 = min(t * per, kFoldBuckets);
+  uint32_t c[per];
+  uint64_t sb[per];
+  uint32_t s = 0, first = kFoldBuckets;
   uint64_t bl = 0;
-  for (uint32_t b = b0; b < b1; ++b) {
-    const uint32_t c = a.cnt[b];
-    s += c;
-    bl += key_sum_blocks(a, b, c);
+#pragma unroll
+  for (uint32_t k = 0; k < per; ++k) c[k] = b0 + k < kFoldBuckets ? a.cnt[b0 + k] : 0u;
+#pragma unroll
+  for (uint32_t k = 0; k < per; ++k) {
+    sb[k] = c[k] ? key_sum_blocks(a, b0 + k, c[k]) : 0ull;
+    s += c[k];
+    bl += sb[k];
+    if (c[k] && first == kFoldBuckets) first = b0 + k;
   }
-  part[t] = s;
-  blk[t] = bl;
+  // inclusive scans of counts and blocks over the wave; the longest chain is the
+  // first non-empty key (lowest key, most blocks)
+  uint32_t si = s;
+  uint64_t bi = bl;
+  uint32_t fm = first;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t v = __shfl_up(si, d);
+    const uint64_t w = (uint64_t)__shfl_up((unsigned long long)bi, d);
+    if (lane >= d) si += v, bi += w;
+    fm = min(fm, (uint32_t)__shfl_xor((int)fm, d));
+  }
+  if (lane == 63) w_cnt[wave] = si, w_blk[wave] = bi;
+  if (lane == 0) w_min[wave] = fm;
   __syncthreads();
-  for (uint32_t d = 1; d < 1024; d <<= 1) {  // inclusive scans of counts and blocks
-    const uint32_t v = t >= d ? part[t - d] : 0u;
-    const uint64_t w = t >= d ? blk[t - d] : 0ull;
-    __syncthreads();
-    part[t] += v;
-    blk[t] += w;
-    __syncthreads();
+  uint32_t lanes = 0, run = si - s, kmax = kFoldBuckets;
+  uint64_t btot = 0, brun = bi - bl;
+  for (uint32_t w = 0; w < 16; ++w) {
+    if (w < wave) run += w_cnt[w], brun += w_blk[w];
+    lanes += w_cnt[w];
+    btot += w_blk[w];
+    kmax = min(kmax, w_min[w]);
   }
-  const uint32_t lanes = part[1023];
-  const uint64_t btot = blk[1023];
-  // longest chain: the first non-empty key (lowest key, most blocks)
-  best[t] = kFoldBuckets;
-  for (uint32_t b = b0; b < b1; ++b)
-    if (a.cnt[b]) {
-      best[t] = b;
-      break;
-    }
-  __syncthreads();
-  for (uint32_t d = 512; d > 0; d >>= 1) {
-    if (t < d) best[t] = min(best[t], best[t + d]);
-    __syncthreads();
-  }
-  const uint32_t kmax = (uint32_t)best[0];
   const uint64_t max_blocks = kmax < kFoldBuckets ? key_max_blocks(a, kmax) : 0;
-  __syncthreads();
   // each thread: the best cut at its buckets' boundaries, packed (cost, key)
-  uint32_t run = part[t] - s;
-  uint64_t brun = blk[t] - bl;
   uint64_t mine = ~0ull;
   uint32_t mine_h = 0;
   // the early head's lanes must be exactly the lanes of >= long_blocks blocks:
   // keys up to that of a long_blocks-block message (fold_key: descending classes)
   const uint32_t klong = a.long_blocks ? fold_key((uint64_t)(a.long_blocks - 1) * 64) + 1 : 0u;
-  for (uint32_t b = b0; b < b1; ++b) {  // cut before bucket b: h = run, its longest = bucket b
-    const uint32_t c = a.cnt[b];
+#pragma unroll
+  for (uint32_t k = 0; k < per; ++k) {  // cut before bucket b: h = run, its longest = bucket b
+    const uint32_t b = b0 + k;
+    if (b >= kFoldBuckets) break;
     if (b == klong) s_long = run;
-    if (c && a.head_cap) {
+    if (c[k] && a.head_cap) {
       const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, key_max_blocks(a, b));
       const uint64_t key = (min(cost, kCostMax) << 20) | b;
       if (key < mine) {
@@ -866,8 +933,8 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
       }
     }
     a.cnt[b] = run;
-    run += c;
-    brun += key_sum_blocks(a, b, c);
+    run += c[k];
+    brun += sb[k];
   }
   if (t == 1023 && a.head_cap) {  // the cut after the last bucket: every lane on the head
     const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, 0);
@@ -877,21 +944,21 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
       mine_h = run;
     }
   }
-  best[t] = mine;
-  part[t] = mine_h;
+  uint64_t wk = mine;
+  for (uint32_t d = 32; d > 0; d >>= 1) wk = min(wk, (uint64_t)__shfl_xor((unsigned long long)wk, d));
+  if (lane == 0) w_key[wave] = wk;
+  if (mine == wk && wk != ~0ull) w_h[wave] = mine_h;  // keys are distinct (the bucket is in them)
   __syncthreads();
-  for (uint32_t d = 512; d > 0; d >>= 1) {
-    if (t < d && best[t + d] < best[t]) {
-      best[t] = best[t + d];
-      part[t] = part[t + d];
-    }
-    __syncthreads();
-  }
+  uint64_t best_key = ~0ull;
+  uint32_t best_h = 0;
+  if (t == 0)
+    for (uint32_t w = 0; w < 16; ++w)
+      if (w_key[w] < best_key) best_key = w_key[w], best_h = w_h[w];
   if (t == 0) {
     // The head's last workgroup has room to spare (a workgroup runs as long as
     // its longest chain): fill it with the next-longest lanes, which would
     // otherwise run as lone chains on the lane kernel (folded c5: 37 -> 128).
-    const uint32_t h = best[0] == ~0ull ? 0u : part[0];
+    const uint32_t h = best_key == ~0ull ? 0u : best_h;
     const uint32_t hfill = (h + a.head_per_wg - 1) / a.head_per_wg * a.head_per_wg;
     const uint32_t late = min(min(hfill, lanes), a.head_cap);
     // an early head (k_fold_longs) is exactly the lanes of >= long_blocks blocks:
@@ -902,14 +969,11 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     // counts ever differ (forced only by the MSHA_FOLD_RACE_TEST build), nothing is
     // skipped: the scan's cut (late head) and the lane kernel hash every lane,
     // the listed ones a second time with the same digests.
-#ifndef MSHA_SCAN_NO_EARLY_CHECK
-    const uint32_t early = a.long_blocks && a.info[4] == s_long ? a.info[4] : 0u;
-#else  // round 5's committed rule, for the check's regression test (tools/r05_race.sh)
-    const uint32_t early = a.long_blocks ? a.info[4] : 0u;
-#endif
+    // (resolved against info[4] by k_fold_scatter: the scan no longer waits for
+    // k_fold_longs, whose head stream the scatter waits for instead)
     a.info[0] = lanes;
-    a.info[1] = early ? early : late;
-    a.info[5] = early ? 0u : late;
+    a.info[16] = s_long;
+    a.info[17] = late;
     PLAN_STAMP(kPsScan, 1);
   }
 }
@@ -922,6 +986,18 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
 __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
   __shared__ uint32_t pos[kFoldBuckets];  // next position of each key the tile holds
   PLAN_STAMP(kPsScatter, 0);
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    // The heads, now that k_fold_longs is done (the stream waited for it after the
+    // scan): the early head's lanes or else the scan's cut (info[17]).
+#ifndef MSHA_SCAN_NO_EARLY_CHECK
+    const uint32_t early = a.long_blocks && a.info[4] == a.info[16] ? a.info[4] : 0u;
+#else  // round 5's committed rule, for the check's regression test (tools/r05_race.sh)
+    const uint32_t early = a.long_blocks ? a.info[4] : 0u;
+#endif
+    const uint32_t late = a.info[17];
+    a.info[1] = early ? early : late;
+    a.info[5] = early ? 0u : late;
+  }
   const uint32_t nk = a.tkcount[blockIdx.x];
   const uint64_t* tl = a.tkeys + (uint64_t)blockIdx.x * kPlanTile;
   for (uint32_t k = threadIdx.x; k < nk; k += blockDim.x) {
@@ -978,7 +1054,7 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
 // LDS, and its threads then claim them side by side (round 4 claimed in the
 // stride loop: every wave's load -> compare chain once per iteration).
 __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
-  if (a.info[6] == 0) return;  // uniform: k_fold_tilescan's first decision
+  if (a.info[6] == 0) return;  // uniform: the first decision (k_fold_tilescan or k_fold_longs_gate)
   __shared__ uint32_t list[kPlanTile];
   __shared__ uint32_t nlist;
   __shared__ unsigned long long s_sum, s_max;
@@ -1105,7 +1181,11 @@ hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
   const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
   const uint64_t cap = a.longs_wgs ? a.longs_wgs : (uint64_t)cus * 4;
   const unsigned grid = (unsigned)std::min<uint64_t>(tiles, cap);
-  const unsigned ggrid = a.gate_wgs ? (unsigned)std::min<uint64_t>(tiles, a.gate_wgs) : grid;
+  // the gate on 64 workgroups unless MSHA_GATE_WGS says otherwise: each ends in
+  // same-address atomics (1,024 of them: ~60 us serialised beside the prefix,
+  // profiles/r06_call4/); partials summed by k_fold_longs instead cost the insert
+  // more bandwidth than they saved (round 6, profiles/r06_plan5/)
+  const unsigned ggrid = (unsigned)std::min<uint64_t>(tiles, a.gate_wgs ? a.gate_wgs : 64u);
   if (a.early_fork) hipLaunchKernelGGL(k_fold_longs_gate, dim3(ggrid), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_longs, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
@@ -1138,17 +1218,17 @@ hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scan_after) {
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scatter_after) {
   if (a.n == 0) return hipSuccess;
   const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
   if (a.table) hipLaunchKernelGGL(k_fold_insert, dim3(ptiles), dim3(256), 0, st, a);
   const unsigned ftiles = (unsigned)((a.n + kFoldTile - 1) / kFoldTile);
   if (!a.table) hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
-  if (scan_after) {
-    const hipError_t e = hipStreamWaitEvent(st, scan_after, 0);
+  hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, a);
+  if (scatter_after) {
+    const hipError_t e = hipStreamWaitEvent(st, scatter_after, 0);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, a);
   hipLaunchKernelGGL(k_fold_scatter, dim3(ftiles), dim3(256), 0, st, a);
   return hipGetLastError();
 }

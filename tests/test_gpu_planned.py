@@ -462,8 +462,8 @@ def test_lookback_folds_as_the_prefix(engine, monkeypatch, capfd, world):
 
 @pytest.mark.parametrize("world", [2, 8])
 def test_early_head_insert_claims_first(engine, monkeypatch, world):
-    """k_fold_scan's defensive check: should the early head's list ever miss a long
-    lane, nothing is skipped. The product kernels cannot reach that state
+    """The planner's defensive check (k_fold_scatter resolves the heads): should the
+    early head's list ever miss a long lane, nothing is skipped. The product kernels cannot reach that state
     (k_fold_longs claims every long message, so it lists every claimant: ADVICE r5),
     so it is forced in a test build only (-DMSHA_FOLD_RACE_TEST; tools/r06_race.sh
     runs this test on one): MSHA_FOLD_LONGS_SKIP_ODD=1 leaves about half the long

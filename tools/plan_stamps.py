@@ -10,8 +10,9 @@ ONE step is stamped; per kernel this prints its span from the step's first stamp
 and per phase the workgroups' durations (p10 / p50 / p90 / max, µs) and their sum
 over workgroups divided by the span (how many workgroups spent the span there).
 
-k_fold_insert's phases: 0 start, 1 off/len loaded, 2 in-tile prefix max, 3 the
-tile look-back (or the tmax read), 4 classified (candidates listed), 5 claims done,
+k_fold_insert's phases: 0 start, 1 off/len loaded, 2 in-tile prefix max (and the
+tile's own post), 3 first pass (fresh so far / candidates listed) and wave 0's
+look-back, 4 second pass (the tiles before applied, lanes counted), 5 claims done,
 6 key16/apairs written, 7 flushed (bucket counters). Words 8/9: candidates, keys.
 
     bash tools/plan_stamps.sh     # builds the variant on the box, then runs this
