@@ -230,9 +230,12 @@ struct FoldArgs {
 // with the early head's list and decision when long_blocks is set; then
 // launch_fold_plan: the insert (or, unfolded, the counts), scan and scatter.
 hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st);
-// scatter_after (may be null): an event k_fold_scatter waits for (the early head's
-// list: the scatter resolves the heads against it).
-hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scatter_after = nullptr);
+// The insert and the scan on st; the scatter on sst (the side stream of the late
+// head: when it is not st, st records `fork` after the scan and sst waits for it),
+// after scatter_after (may be null: the early head's list, against which the scatter
+// resolves the heads).
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipStream_t sst, hipEvent_t fork,
+                            hipEvent_t scatter_after);
 // The early head's list (FoldArgs::longs): on a stream of its own, after the
 // prefix, beside the alias insert (both claim through the same table).
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st);

@@ -2904,17 +2904,19 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // resident before the lane kernel fills every SIMD (queued the other way
     // round, the head could not get a CU's registers until the lane kernel
     // drained: c5 folded 6.2 ms, its 1,427-block chain starting at the end).
-    hipStream_t ps = st;
+    // Round 6: the memsets, the insert and the scan run on the caller's stream, and
+    // the side stream joins at the scatter (with the early head's list), so a step
+    // starts without a cross-queue hand-off (~20 us of a folded c5 step's timeline,
+    // profiles/r06_plan7/).
+    hipStream_t ps = st;  // the scatter's and the late head's
     if (head) {
       if (!d.side_stream) HIPCHK(hipStreamCreateWithFlags(&d.side_stream, hipStreamNonBlocking));
       for (hipEvent_t* e : {&d.ev_fork, &d.ev_fplan, &d.ev_join})
         if (!*e) HIPCHK(hipEventCreateWithFlags(e, hipEventDisableTiming));
-      HIPCHK(hipEventRecord(d.ev_fork, st));
-      HIPCHK(hipStreamWaitEvent(d.side_stream, d.ev_fork, 0));
       ps = d.side_stream;
     }
-    if (clear_table) HIPCHK(hipMemsetAsync(d.f_table.p, 0, d.f_table.cap, ps));
-    HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, fold_zero, ps));
+    if (clear_table) HIPCHK(hipMemsetAsync(d.f_table.p, 0, d.f_table.cap, st));
+    HIPCHK(hipMemsetAsync(d.f_cnt.p, 0, fold_zero, st));
     // (the order's positions past the last lane are filled by k_fold_scatter)
     msha::FoldArgs fa;
     fa.off = d_off;
@@ -3007,15 +3009,15 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.longs_wgs = (uint32_t)env_u64("MSHA_LONGS_WGS", 0);
     fa.gate_wgs = (uint32_t)env_u64("MSHA_GATE_WGS", 0);
     if (fa.early_fork) {
-      HIPCHK(hipEventRecord(d.ev_longs, ps));
+      HIPCHK(hipEventRecord(d.ev_longs, st));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
     }
-    HIPCHK(msha::launch_fold_prefix(fa, ps));
+    HIPCHK(msha::launch_fold_prefix(fa, st));
     if (early) {
       // the list runs beside the tile prefix (forked) or after it, and beside the
       // alias insert
       if (!fa.early_fork) {
-        HIPCHK(hipEventRecord(d.ev_longs, ps));
+        HIPCHK(hipEventRecord(d.ev_longs, st));
         HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
       }
       HIPCHK(msha::launch_fold_longs(fa, d.cus, d.head_stream));
@@ -3032,7 +3034,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
       count_launch(ctx, nullptr, ek);
       HIPCHK(hipEventRecord(d.ev_join2, d.head_stream));
     }
-    HIPCHK(msha::launch_fold_plan(fa, ps, early ? d.ev_longs : nullptr));
+    HIPCHK(msha::launch_fold_plan(fa, st, ps, d.ev_fork, early ? d.ev_longs : nullptr));
     const uint32_t* order = d.f_order.as<uint32_t>();
     msha::LaunchKind kind;
     if (all_coop) {

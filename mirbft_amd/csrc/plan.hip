@@ -68,6 +68,13 @@ __device__ __forceinline__ void plan_stamp_val(uint32_t kind, uint32_t w, uint64
 #define PLAN_STAMP_VAL(kind, w, v)
 #endif
 
+// A wave-uniform lane's value (every use here names a lane found by a ballot):
+// v_readlane, where __shfl is a ds_bpermute through the LDS crossbar -- the
+// planner's LDS is busy enough with its atomics.
+__device__ __forceinline__ uint32_t lane_value(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+
 __device__ __forceinline__ uint64_t dev_blocks_for(uint64_t len) { return (len >> 6) + ((len & 63) < 56 ? 1 : 2); }
 
 __device__ __forceinline__ uint64_t plan_hash(uint64_t off, uint64_t len) {
@@ -163,7 +170,7 @@ __device__ __forceinline__ void wave_count(TileTable& t, uint32_t* gcnt, uint32_
   const unsigned lane = __lane_id();
   while (pend) {
     const int leader = __ffsll((long long)pend) - 1;
-    const uint32_t k0 = __shfl(k, leader);
+    const uint32_t k0 = lane_value(k, leader);
     const uint64_t same = __ballot(valid && k == k0) & pend;
     uint32_t j = 0, base = 0;
     if ((int)lane == leader) {
@@ -177,8 +184,8 @@ __device__ __forceinline__ void wave_count(TileTable& t, uint32_t* gcnt, uint32_
         if (kMinAux) atomicMin(&gmin[k0 / B], idx);
       }
     }
-    j = __shfl(j, leader);
-    base = __shfl(base, leader);
+    j = lane_value(j, leader);
+    base = lane_value(base, leader);
     if ((same >> lane) & 1) done(j, base + (uint32_t)__popcll(same & ((1ull << lane) - 1)));
     pend &= ~same;
   }
@@ -524,7 +531,7 @@ __device__ __forceinline__ void fold_hist_add_wave(FoldHist& h, bool valid, uint
   const uint32_t k = valid ? fold_key(len) : 0xFFFFFFFFu;
   const uint64_t any = __ballot(valid);
   if (!any) return;
-  const uint32_t k0 = __shfl(k, __ffsll((long long)any) - 1);
+  const uint32_t k0 = lane_value(k, __ffsll((long long)any) - 1);
   const uint64_t same = __ballot(valid && k == k0);
   const unsigned lane = __lane_id();
   if ((same >> lane) & 1) {
@@ -540,7 +547,7 @@ __device__ __forceinline__ void fold_hist_add_wave_key(const FoldArgs& a, FoldHi
                                                        uint64_t i) {
   const uint64_t any = __ballot(valid);
   if (!any) return;
-  const uint32_t k0 = __shfl(k, __ffsll((long long)any) - 1);
+  const uint32_t k0 = lane_value(k, __ffsll((long long)any) - 1);
   const uint64_t same = __ballot(valid && k == k0);
   const unsigned lane = __lane_id();
   if ((same >> lane) & 1) {
@@ -592,25 +599,33 @@ __device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h, 
 // folding -- and counts itself in tstat[tiles] (tests expect 0).
 constexpr uint64_t kTileAgg = 1ull << 62, kTileIncl = 2ull << 62, kTileVal = kTileAgg - 1;
 constexpr uint32_t kLookbackSpins = 1u << 16;
+__device__ __forceinline__ uint64_t tile_lookback_give_up(const FoldArgs& a) {
+  if (__lane_id() == 0) {
+    const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&a.tstat[tiles]), 1ull);
+  }
+  return kTileVal;
+}
 __device__ __forceinline__ uint64_t tile_lookback(const FoldArgs& a, uint64_t tile) {
+#ifdef MSHA_LOOKBACK_GIVEUP_TEST  // test build only (tests/test_gpu_planned.py, tools/r06_race.sh)
+  if (tile % 3 == 1) return tile_lookback_give_up(a);
+#endif
   const unsigned lane = __lane_id();
   uint64_t acc = 0;
   uint32_t spins = 0;
   for (int64_t hi = (int64_t)tile - 1; hi >= 0; hi -= 64) {
     const int64_t j = hi - (int64_t)lane;  // lane 0 the nearest tile
     uint64_t v = j >= 0 ? __hip_atomic_load(&a.tstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : kTileIncl;
-    while (__ballot(v == 0)) {
-      if (++spins > kLookbackSpins) {
-        if (lane == 0) {
-          const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
-          atomicAdd(reinterpret_cast<unsigned long long*>(&a.tstat[tiles]), 1ull);
-        }
-        return kTileVal;
-      }
+    uint64_t incl;
+    for (;;) {  // until every tile up to the nearest inclusive post has posted
+      const uint64_t ready = __ballot(v != 0);
+      incl = __ballot((v & ~kTileVal) == kTileIncl);
+      const uint64_t need = incl ? ((incl & (0ull - incl)) << 1) - 1 : ~0ull;
+      if ((ready & need) == need) break;
+      if (++spins > kLookbackSpins) return tile_lookback_give_up(a);
       __builtin_amdgcn_s_sleep(2);
       if (v == 0) v = __hip_atomic_load(&a.tstat[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    const uint64_t incl = __ballot((v & ~kTileVal) == kTileIncl);
     const int stop = incl ? __ffsll((long long)incl) - 1 : 63;  // lanes 0..stop count
     uint64_t x = (int)lane <= stop ? (v & kTileVal) : 0ull;
     for (uint32_t d = 32; d > 0; d >>= 1) x = max(x, (uint64_t)__shfl_xor(x, d));
@@ -699,7 +714,7 @@ __global__ __launch_bounds__(256, 4) void k_fold_insert(FoldArgs a) {
       uint32_t at = 0;
       const int leader = __ffsll((long long)cm) - 1;
       if ((int)lane == leader) at = atomicAdd(&ncand, (uint32_t)__popcll(cm));
-      at = __shfl(at, leader);
+      at = lane_value(at, leader);
       if (is_cand) cand[at + (uint32_t)__popcll(cm & ((1ull << lane) - 1))] = (uint16_t)(lb + r);
     }
     run = max(run, o[r]);
@@ -736,7 +751,7 @@ __global__ __launch_bounds__(256, 4) void k_fold_insert(FoldArgs a) {
       uint32_t at = 0;
       const int leader = __ffsll((long long)cm) - 1;
       if ((int)lane == leader) at = atomicAdd(&ncand, (uint32_t)__popcll(cm));
-      at = __shfl(at, leader);
+      at = lane_value(at, leader);
       if (demoted) cand[at + (uint32_t)__popcll(cm & ((1ull << lane) - 1))] = (uint16_t)(lb + r);
     }
   }
@@ -765,7 +780,7 @@ __global__ __launch_bounds__(256, 4) void k_fold_insert(FoldArgs a) {
       uint32_t at = 0;
       const int leader = __ffsll((long long)fm) - 1;
       if ((int)lane == leader) at = atomicAdd(&nalias, (uint32_t)__popcll(fm));
-      at = __shfl(at, leader);
+      at = lane_value(at, leader);
       if (folded) a.apairs[tile0 + at + (uint32_t)__popcll(fm & ((1ull << lane) - 1))] = ((uint64_t)rp << 32) | (uint32_t)i;
     }
   }
@@ -1018,12 +1033,12 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
     // on one LDS word serialise. The rest one each, as before.
     const uint64_t any = __ballot(valid);
     if (!any) continue;
-    const uint32_t k0 = __shfl(k, __ffsll((long long)any) - 1);
+    const uint32_t k0 = lane_value(k, __ffsll((long long)any) - 1);
     const uint64_t same = __ballot(valid && k == k0);
     const uint32_t before = (uint32_t)__popcll(same & ((1ull << lane) - 1));
     uint32_t b0 = 0;
     if (((same >> lane) & 1) && before == 0) b0 = atomicAdd(&pos[k0], (uint32_t)__popcll(same));
-    b0 = __shfl(b0, __ffsll((long long)same) - 1);
+    b0 = lane_value(b0, __ffsll((long long)same) - 1);
     if ((same >> lane) & 1)
       a.order[b0 + before] = (uint32_t)i;
     else if (valid)
@@ -1081,7 +1096,7 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
         uint32_t at = 0;
         const int leader = __ffsll((long long)lm) - 1;
         if ((int)lane == leader) at = atomicAdd(&nlist, (uint32_t)__popcll(lm));
-        at = __shfl(at, leader);
+        at = lane_value(at, leader);
         if (lng) list[at + (uint32_t)__popcll(lm & ((1ull << lane) - 1))] = (uint32_t)(base + r);
       }
     }
@@ -1197,10 +1212,14 @@ __global__ __launch_bounds__(256) void k_fold_fill(FoldArgs a, uint8_t* __restri
   PLAN_STAMP(kPsFill, 0);
   const uint64_t tiles = (a.n + kPlanTile - 1) / kPlanTile;
   for (uint64_t tile = blockIdx.x; tile < tiles; tile += gridDim.x) {
-    const uint32_t cnt = a.acount[tile];
     const uint64_t* p = a.apairs + tile * kPlanTile;
+    // the first pair loads beside the count (a tile's segment holds kPlanTile
+    // entries, inside the batch): two dependent memory trips a pair, not three
+    const bool in = tile * kPlanTile + threadIdx.x < a.n;
+    const uint64_t v0 = in ? p[threadIdx.x] : 0ull;
+    const uint32_t cnt = a.acount[tile];
     for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
-      const uint64_t v = p[k];
+      const uint64_t v = k == threadIdx.x ? v0 : p[k];
       const uint4* src = reinterpret_cast<const uint4*>(out + 32 * (v >> 32));
       uint4* dst = reinterpret_cast<uint4*>(out + 32 * (v & 0xFFFFFFFFull));
       dst[0] = src[0];
@@ -1218,18 +1237,24 @@ hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
-hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipEvent_t scatter_after) {
+hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipStream_t sst, hipEvent_t fork,
+                            hipEvent_t scatter_after) {
   if (a.n == 0) return hipSuccess;
   const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
   if (a.table) hipLaunchKernelGGL(k_fold_insert, dim3(ptiles), dim3(256), 0, st, a);
   const unsigned ftiles = (unsigned)((a.n + kFoldTile - 1) / kFoldTile);
   if (!a.table) hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, a);
-  if (scatter_after) {
-    const hipError_t e = hipStreamWaitEvent(st, scatter_after, 0);
+  if (sst != st) {
+    hipError_t e = hipEventRecord(fork, st);
+    if (e == hipSuccess) e = hipStreamWaitEvent(sst, fork, 0);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(k_fold_scatter, dim3(ftiles), dim3(256), 0, st, a);
+  if (scatter_after) {
+    const hipError_t e = hipStreamWaitEvent(sst, scatter_after, 0);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(k_fold_scatter, dim3(ftiles), dim3(256), 0, sst, a);
   return hipGetLastError();
 }
 

@@ -460,6 +460,25 @@ def test_lookback_folds_as_the_prefix(engine, monkeypatch, capfd, world):
     assert lanes["1"] == lanes["0"] and 0 < lanes["1"] < w.n, lanes
 
 
+def test_lookback_give_up_exact(engine, monkeypatch):
+    """The tile look-back's give-up path (plan.hip tile_lookback: after a bounded wait a
+    tile takes the largest threshold, so none of its messages -- nor, through its post,
+    any later tile's -- is fresh and every one claims in the alias table): the digests
+    stay exact, and MSHA_CHECK_LOOKBACK reports it. The product kernels only take it
+    when a wait outlasts 2^16 polls, so a -DMSHA_LOOKBACK_GIVEUP_TEST build forces it on
+    every third tile (tools/r06_race.sh). A c5 slice."""
+    from mirbft_amd import _lib
+    if "-DMSHA_LOOKBACK_GIVEUP_TEST" not in _lib.build_id()["flags"].split():
+        pytest.skip("needs a -DMSHA_LOOKBACK_GIVEUP_TEST build (tools/r06_race.sh)")
+    w = W.c5_storm(n=(1 << 23) // 8)
+    exp = _expect(w)
+    monkeypatch.setenv("MSHA_CHECK_LOOKBACK", "0")
+    assert np.array_equal(_run(engine, w, True), exp)
+    monkeypatch.setenv("MSHA_CHECK_LOOKBACK", "1")
+    with pytest.raises(MshaError, match="look-back gave up"):
+        _run(engine, w, True)
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_early_head_insert_claims_first(engine, monkeypatch, world):
     """The planner's defensive check (k_fold_scatter resolves the heads): should the

@@ -16,3 +16,8 @@ echo "with the check (expected: pass): rc=$?"; tail -1 $OUT/check.txt
 MSHA_LIB_PATH=/tmp/msha_ab/race_nocheck.so MSHA_ALLOW_FOREIGN_LIB=1 timeout -k 10 300 python -u -m pytest \
   tests/test_gpu_planned.py -m gpu -q -k insert_claims_first --timeout 200 --timeout-method thread > $OUT/nocheck.txt 2>&1
 echo "without the check (expected: fail): rc=$?"; tail -1 $OUT/nocheck.txt
+# the tile look-back's give-up path, forced on every third tile (expected: pass)
+timeout -k 10 300 bash tools/ab_build.sh giveup -DMSHA_LOOKBACK_GIVEUP_TEST >> $OUT/build.log 2>&1 || { tail $OUT/build.log; exit 1; }
+MSHA_LIB_PATH=/tmp/msha_ab/giveup.so MSHA_ALLOW_FOREIGN_LIB=1 timeout -k 10 300 python -u -m pytest tests/test_gpu_planned.py \
+  -m gpu -q -k lookback_give_up --timeout 200 --timeout-method thread > $OUT/giveup.txt 2>&1
+echo "look-back give-up (expected: pass): rc=$?"; tail -1 $OUT/giveup.txt
