@@ -523,26 +523,12 @@ __device__ __forceinline__ void fold_hist_add(FoldHist& h, uint64_t len) {
   atomicAdd(&h.n[k], 1u);
   fold_hist_big(h, k, blocks);
 }
-// The same over the active lanes of a wave where valid: the lanes sharing the
-// first valid lane's key add once, together (a storm's wave: ~70 % one key,
-// which one LDS atomic per lane serialises ~45 deep), the rest one each.
-__device__ __forceinline__ void fold_hist_add_wave(FoldHist& h, bool valid, uint64_t len) {
-  const uint64_t blocks = dev_blocks_for(len);
-  const uint32_t k = valid ? fold_key(len) : 0xFFFFFFFFu;
-  const uint64_t any = __ballot(valid);
-  if (!any) return;
-  const uint32_t k0 = lane_value(k, __ffsll((long long)any) - 1);
-  const uint64_t same = __ballot(valid && k == k0);
-  const unsigned lane = __lane_id();
-  if ((same >> lane) & 1) {
-    if ((same & ((1ull << lane) - 1)) == 0) atomicAdd(&h.n[k0], (uint32_t)__popcll(same));
-  } else if (valid) {
-    atomicAdd(&h.n[k], 1u);
-  }
-  if (valid) fold_hist_big(h, k, blocks);
-}
-// The same by key, for message i (its length is read again only for the rare
-// power-of-two classes, whose block counts the head's cost model needs exactly).
+// Over a wave's valid lanes by key, for message i: the lanes sharing the first
+// valid lane's key add once, together (a storm's wave: ~70 % one key, which one
+// LDS atomic per lane serialises ~45 deep), the rest one each -- a loop of one
+// atomic per distinct key measured far slower (exact-length classes: many keys a
+// wave; profiles/r06_plan9/). The length is read again only for the rare
+// power-of-two classes, whose block counts the head's cost model needs exactly.
 __device__ __forceinline__ void fold_hist_add_wave_key(const FoldArgs& a, FoldHist& h, bool valid, uint32_t k,
                                                        uint64_t i) {
   const uint64_t any = __ballot(valid);
@@ -1001,6 +987,14 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
 __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
   __shared__ uint32_t pos[kFoldBuckets];  // next position of each key the tile holds
   PLAN_STAMP(kPsScatter, 0);
+  const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
+  // Round 6: the thread's 16 keys load first, unconditionally (a clamped index),
+  // beside the bucket starts below: a guarded load per row compiled to a branch
+  // and a wait on each, 16 memory round trips one after another (the order loop's
+  // ~11 us a workgroup, profiles/r06_plan7/ stamps)
+  uint32_t kr[kFoldItems];
+#pragma unroll
+  for (uint32_t r = 0; r < kFoldItems; ++r) kr[r] = a.key16[min(base + r * 256 + threadIdx.x, a.n - 1)];
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     // The heads, now that k_fold_longs is done (the stream waited for it after the
     // scan): the early head's lanes or else the scan's cut (info[17]).
@@ -1021,18 +1015,18 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
   }
   __syncthreads();
   PLAN_STAMP(kPsScatter, 1);
-  const uint64_t base = (uint64_t)blockIdx.x * kFoldTile;
-  const unsigned lane = __lane_id();
 #pragma unroll
   for (uint32_t r = 0; r < kFoldItems; ++r) {
     const uint64_t i = base + r * 256 + threadIdx.x;
-    const uint32_t k = i < a.n ? a.key16[i] : 0xFFFFu;
+    const uint32_t k = i < a.n ? kr[r] : 0xFFFFu;
     const bool valid = k != 0xFFFFu;
     // Round 6: the lanes sharing the first valid lane's key (a storm's wave: ~70 %
     // one key) take their positions with ONE LDS atomic, ranked by lane; 64 atomics
-    // on one LDS word serialise. The rest one each, as before.
+    // on one LDS word serialise. The rest one each, as before (one atomic per
+    // distinct key measured far slower: profiles/r06_plan9/).
     const uint64_t any = __ballot(valid);
     if (!any) continue;
+    const unsigned lane = __lane_id();
     const uint32_t k0 = lane_value(k, __ffsll((long long)any) - 1);
     const uint64_t same = __ballot(valid && k == k0);
     const uint32_t before = (uint32_t)__popcll(same & ((1ull << lane) - 1));
@@ -1215,15 +1209,15 @@ __global__ __launch_bounds__(256) void k_fold_fill(FoldArgs a, uint8_t* __restri
     const uint64_t* p = a.apairs + tile * kPlanTile;
     // the first pair loads beside the count (a tile's segment holds kPlanTile
     // entries, inside the batch): two dependent memory trips a pair, not three
-    const bool in = tile * kPlanTile + threadIdx.x < a.n;
-    const uint64_t v0 = in ? p[threadIdx.x] : 0ull;
+    const uint64_t v0 = a.apairs[min(tile * kPlanTile + threadIdx.x, a.n - 1)];  // unconditional: no branch
     const uint32_t cnt = a.acount[tile];
     for (uint32_t k = threadIdx.x; k < cnt; k += blockDim.x) {
       const uint64_t v = k == threadIdx.x ? v0 : p[k];
       const uint4* src = reinterpret_cast<const uint4*>(out + 32 * (v >> 32));
       uint4* dst = reinterpret_cast<uint4*>(out + 32 * (v & 0xFFFFFFFFull));
-      dst[0] = src[0];
-      dst[1] = src[1];
+      const uint4 x0 = src[0], x1 = src[1];  // both loads before either store (out may alias)
+      dst[0] = x0;
+      dst[1] = x1;
     }
   }
   PLAN_STAMP(kPsFill, 1);
