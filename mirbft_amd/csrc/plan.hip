@@ -578,11 +578,13 @@ __device__ __forceinline__ void fold_hist_flush(const FoldArgs& a, FoldHist& h, 
 // its own. A post is 62 bits of offset (an arena offset past 2^62 bytes is
 // clamped: the threshold then only folds less) and 2 bits of state; 0 = not yet.
 //
-// Waiting is on earlier tiles only, which the dispatcher has placed before this
-// one (in order on each XCD), so it ends; still, a look-back that has waited
-// kLookbackSpins polls gives up and returns the largest threshold, under which no
-// message is fresh and every one claims in the table -- the same digests, less
-// folding -- and counts itself in tstat[tiles] (tests expect 0).
+// Waiting is on earlier tiles only, and a tile posts its own offset before it
+// waits: the lowest unposted tile waits on nobody, and each XCD dispatches its
+// tiles in order, so that tile is resident or next in line and the look-backs end.
+// Still, one that has waited kLookbackSpins polls gives up and returns the largest
+// threshold, under which no message is fresh and every one claims in the table --
+// the same digests, less folding -- and counts itself in tstat[tiles] (tests expect
+// 0; a -DMSHA_LOOKBACK_GIVEUP_TEST build forces it, tools/r06_race.sh).
 constexpr uint64_t kTileAgg = 1ull << 62, kTileIncl = 2ull << 62, kTileVal = kTileAgg - 1;
 constexpr uint32_t kLookbackSpins = 1u << 16;
 __device__ __forceinline__ uint64_t tile_lookback_give_up(const FoldArgs& a) {
