@@ -46,6 +46,9 @@ enum LaunchKind { kLaunchNone = 0, kLaunchLane, kLaunchPipe, kLaunchCoop, kLaunc
 // past *head idle) or the rest (lanes below *head idle); neither splits.
 constexpr uint32_t kNoLane = 0xFFFFFFFFu;
 constexpr uint32_t kWsSlots = 64, kWsStride = 16;  // work-stealing tile counters, 64 B apart
+// The planner's two-level grid reductions (plan.hip grid_reduce_last): 16 group
+// slots and a top slot, 64 B each, zeroed words
+constexpr uint32_t kGridGroups = 16, kGridWords = (kGridGroups + 1) * 16;
 struct LaneGate {
   const uint32_t* head = nullptr;
   bool head_part = false;
@@ -152,6 +155,8 @@ struct FoldArgs {
   // tile_lookback) -- no k_fold_tilemax / k_fold_tilescan; then one more zeroed
   // word: look-backs that gave up waiting (0 expected; see tile_lookback)
   uint64_t* tstat = nullptr;
+  // 2 x kGridWords zeroed words: k_fold_longs' then k_fold_longs_gate's grid reduction
+  uint32_t* grid_ws = nullptr;
   uint32_t* cnt;              // kFoldBuckets zeroed counters (by key) -> bucket starts
   uint64_t* big = nullptr;    // 2 x kFoldBigBuckets zeroed: per power-of-two key, the largest
                               // block count and the block sum (the head's cost model needs the
@@ -167,12 +172,11 @@ struct FoldArgs {
   uint64_t* tkeys = nullptr;
   uint32_t* tkcount = nullptr;
   uint32_t* info;             // [0] lanes, [1] positions the lane kernel skips (the head's),
-                              // [2] distinct long payloads, [3] k_fold_longs workgroups done,
+                              // [2] distinct long payloads, [3] unused,
                               // [4] the early head's lanes (0: none), [5] the late head's,
                               // [6] the first decision (0: no early head), by k_fold_tilescan,
-                              // or with early_fork by k_fold_longs_gate ([7]: its workgroups
-                              // done, [12..15] two u64: the short blocks and longest chain),
-                              // [8..11] two u64: the batch's blocks and longest chain,
+                              // or with early_fork by k_fold_longs_gate, [7..15] unused (the
+                              // list's and the gate's sums: grid_ws),
                               // [16] lanes of >= long_blocks blocks, [17] the scan's cut (the
                               // scatter resolves [1] and [5] from them and [4])
                               // (all 32 words zeroed by the caller)

@@ -2854,15 +2854,15 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // then FoldArgs::big -- cleared by ONE memset per call
     // (+ the work-stealing lane kernel's tile counters)
     const uint64_t fold_zero_fixed = 128 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets +
-                                     4 * msha::kWsSlots * msha::kWsStride;
+                                     4 * msha::kWsSlots * msha::kWsStride + 4 * 2 * msha::kGridWords;
     // Round 6: a folded call's insert finds its tile prefix by look-back (plan.hip
     // tile_lookback) over status words zeroed with the rest -- no k_fold_tilemax /
     // k_fold_tilescan and their two dependent launches. MSHA_FOLD_LOOKBACK=0: the
     // two-kernel prefix (A/B).
     const bool lookback = fold && env_u64("MSHA_FOLD_LOOKBACK", 1) != 0;
     const uint64_t ptiles = (n + 4095) / 4096;
-    static_assert((128 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets + 4 * msha::kWsSlots * msha::kWsStride) %
-                      8 == 0,
+    static_assert((128 + 4 * msha::kFoldBuckets + 16 * msha::kFoldBigBuckets + 4 * msha::kWsSlots * msha::kWsStride +
+                   4 * 2 * msha::kGridWords) % 8 == 0,
                   "the look-back's status words follow 8-byte aligned");
     // (a multiple of 64 bytes: an unaligned tail made hipMemsetAsync a second fill kernel)
     const uint64_t fold_zero = (fold_zero_fixed + (lookback ? 8 * (ptiles + 1) : 0) + 63) / 64 * 64;
@@ -2938,6 +2938,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     fa.big = reinterpret_cast<uint64_t*>(fa.cnt + msha::kFoldBuckets);  // kFoldBuckets is even: 8-byte aligned
     fa.order = d.f_order.as<uint32_t>();
     fa.tstat = lookback ? reinterpret_cast<uint64_t*>(d.f_cnt.as<uint8_t>() + fold_zero_fixed) : nullptr;
+    fa.grid_ws = reinterpret_cast<uint32_t*>(fa.big + 2 * msha::kFoldBigBuckets) + msha::kWsSlots * msha::kWsStride;
     fa.simds = (uint32_t)d.cus * 4;
     // The head's kernel. Folded, a head is the few distinct long payloads: the
     // two-lane chain (k_digest_chain2, 64 messages per CU, ~10 % fewer cycles a

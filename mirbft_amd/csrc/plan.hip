@@ -1048,6 +1048,41 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
   PLAN_STAMP(kPsScatter, 3);
 }
 
+// A grid's (sum, max) and "am I the last workgroup" without one hot word (round 6:
+// each of k_fold_longs' and k_fold_longs_gate's 256-1,024 workgroups ended in three
+// atomics on the same words, serialised at ~20 ns each -- ~23 us of an N = 8 rank's
+// 65 us before its chain starts, profiles/r06_n8_trace/). Workgroup w adds to group
+// w mod G's slots and counts itself there; a group's last workgroup adds the group's
+// totals to the top slots and counts the group; the last group's last workgroup
+// returns true with the grid's totals. Thread 0 only. ws: kGridWords zeroed words,
+// one 64-byte slot a group ([0] count, [2..3] sum, [4..5] max), then the top slot.
+__device__ __forceinline__ bool grid_reduce_last(uint32_t* ws, uint64_t sum, uint64_t mx, uint64_t& tot,
+                                                 uint64_t& top_max) {
+  const uint32_t groups = min(gridDim.x, kGridGroups);
+  const uint32_t g = blockIdx.x % groups;
+  uint32_t* gs = ws + g * 16;
+  unsigned long long* gsum = reinterpret_cast<unsigned long long*>(gs + 2);
+  unsigned long long* gmax = reinterpret_cast<unsigned long long*>(gs + 4);
+  atomicAdd(gsum, (unsigned long long)sum);
+  atomicMax(gmax, (unsigned long long)mx);
+  __threadfence();  // this workgroup's results (and sums) before its count
+  if (atomicAdd(&gs[0], 1u) != (gridDim.x - g + groups - 1) / groups - 1) return false;
+  __threadfence();
+  const uint64_t s = __hip_atomic_load(gsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t m = __hip_atomic_load(gmax, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint32_t* top = ws + kGridGroups * 16;
+  unsigned long long* tsum = reinterpret_cast<unsigned long long*>(top + 2);
+  unsigned long long* tmx = reinterpret_cast<unsigned long long*>(top + 4);
+  atomicAdd(tsum, (unsigned long long)s);
+  atomicMax(tmx, (unsigned long long)m);
+  __threadfence();
+  if (atomicAdd(&top[0], 1u) != groups - 1) return false;
+  __threadfence();
+  tot = __hip_atomic_load(tsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  top_max = __hip_atomic_load(tmx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
 // The early head's list: every message of >= long_blocks blocks claims its
 // (off, len) in the alias table (a hot payload costs a cached read after the
 // first claim); each claimant -- one per distinct long payload -- is listed. It
@@ -1069,7 +1104,6 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
   __shared__ uint32_t list[kPlanTile];
   __shared__ uint32_t nlist;
   __shared__ unsigned long long s_sum, s_max;
-  __shared__ bool last;
   if (threadIdx.x == 0) s_sum = s_max = 0;
   uint64_t sum = 0, mx = 0;
   const unsigned lane = __lane_id();
@@ -1114,19 +1148,9 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
   atomicAdd(&s_sum, (unsigned long long)sum);
   atomicMax(&s_max, (unsigned long long)mx);
   __syncthreads();
-  unsigned long long* g = reinterpret_cast<unsigned long long*>(a.info + 8);  // [blocks, longest]
-  if (threadIdx.x == 0) {
-    atomicAdd(&g[0], s_sum);
-    atomicMax(&g[1], s_max);
-    __threadfence();  // this workgroup's list entries and sums before its count
-    last = atomicAdd(&a.info[3], 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __threadfence();
+  uint64_t tot = 0, lng = 0;
+  if (threadIdx.x == 0 && grid_reduce_last(a.grid_ws, s_sum, s_max, tot, lng)) {  // (its fences cover the list)
     const uint32_t c = __hip_atomic_load(&a.info[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t tot = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t lng = __hip_atomic_load(&g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t_body = tot * a.wave_block_cycles / (64ull * a.simds);
     const uint64_t t_head = lng * a.early_cycles;
     a.info[4] = c <= a.long_cap && t_body < t_head ? c : 0u;
@@ -1140,7 +1164,6 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
 // stream, forked right after the planner's memsets, beside k_fold_tilemax.
 __global__ __launch_bounds__(256) void k_fold_longs_gate(FoldArgs a) {
   __shared__ unsigned long long s_sum, s_max;
-  __shared__ bool last;
   PLAN_STAMP(kPsGate, 0);
   if (threadIdx.x == 0) s_sum = s_max = 0;
   __syncthreads();
@@ -1166,18 +1189,8 @@ __global__ __launch_bounds__(256) void k_fold_longs_gate(FoldArgs a) {
     atomicMax(&s_max, (unsigned long long)mx);
   }
   __syncthreads();
-  unsigned long long* g = reinterpret_cast<unsigned long long*>(a.info + 12);  // [short blocks, longest]
-  if (threadIdx.x == 0) {
-    atomicAdd(&g[0], s_sum);
-    atomicMax(&g[1], s_max);
-    __threadfence();  // this workgroup's sums before its count
-    last = atomicAdd(&a.info[7], 1u) == gridDim.x - 1;
-  }
-  __syncthreads();
-  if (last && threadIdx.x == 0) {
-    __threadfence();
-    const uint64_t ss = __hip_atomic_load(&g[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t sm = __hip_atomic_load(&g[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  uint64_t ss = 0, sm = 0;
+  if (threadIdx.x == 0 && grid_reduce_last(a.grid_ws + kGridWords, s_sum, s_max, ss, sm)) {
     const uint64_t t_body = ss * a.wave_block_cycles / (64ull * a.simds);
     const uint64_t t_head = sm * a.early_cycles;
     a.info[6] = sm >= a.long_blocks && t_body < t_head ? 1u : 0u;
@@ -1196,7 +1209,10 @@ hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st) {
   // same-address atomics (1,024 of them: ~60 us serialised beside the prefix,
   // profiles/r06_call4/); partials summed by k_fold_longs instead cost the insert
   // more bandwidth than they saved (round 6, profiles/r06_plan5/)
-  const unsigned ggrid = (unsigned)std::min<uint64_t>(tiles, a.gate_wgs ? a.gate_wgs : 64u);
+  // (a batch of at most a tile a CU: one workgroup a tile -- an N = 8 rank's gate ran
+  // its 4 tiles a workgroup one after another, 27 us before the list could start)
+  const unsigned ggrid = (unsigned)std::min<uint64_t>(
+      tiles, a.gate_wgs ? a.gate_wgs : (tiles <= (uint64_t)cus ? (uint64_t)cus : 64u));
   if (a.early_fork) hipLaunchKernelGGL(k_fold_longs_gate, dim3(ggrid), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_longs, dim3(grid), dim3(256), 0, st, a);
   return hipGetLastError();
