@@ -178,7 +178,8 @@ struct FoldArgs {
                               // or with early_fork by k_fold_longs_gate, [7..15] unused (the
                               // list's and the gate's sums: grid_ws),
                               // [16] lanes of >= long_blocks blocks, [17] the scan's cut (the
-                              // scatter resolves [1] and [5] from them and [4])
+                              // scatter resolves [1] and [5] from them and [4]), [20] / [21]
+                              // (early_only) the eight- / two-lane early head's lanes
                               // (all 32 words zeroed by the caller)
   // The early head (folding only; long_blocks 0: off): k_fold_tilescan sizes the
   // batch (info[6]: 0 when the short messages alone outlast the longest chain);
@@ -205,6 +206,15 @@ struct FoldArgs {
   uint32_t ws_long = 0;
   uint32_t longs_wgs = 0;  // k_fold_longs / k_fold_longs_gate workgroups (0: 4 a CU; A/B MSHA_LONGS_WGS)
   uint32_t gate_wgs = 0;   // k_fold_longs_gate's workgroups (0: 64; MSHA_GATE_WGS)
+  // (early_fork, A/B MSHA_EARLY_ONLY) the early head takes every distinct long payload
+  // the list holds: info[20] arms the eight-lane launch (its chain the long pole),
+  // info[21] the two-lane one; no late head (the scatter leaves info[1] = the early
+  // head's lanes or 0)
+  uint32_t early_only = 0;
+  // Round 6: the insert's claims list the early head (every claimant of >= long_blocks
+  // blocks) and the scan decides it (info[4], [20], [21]): no k_fold_longs_gate /
+  // k_fold_longs pass beside the insert; implies early_only
+  uint32_t insert_list = 0;
   uint32_t long_cap = 0;
   uint32_t head_cap = 0;      // 0: no head
   uint32_t simds = 1024;
@@ -238,8 +248,10 @@ hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st);
 // head: when it is not st, st records `fork` after the scan and sst waits for it),
 // after scatter_after (may be null: the early head's list, against which the scatter
 // resolves the heads).
+// after_scan (may be null): recorded on st right after the scan (the early head's
+// stream waits for it when the insert lists the early head: FoldArgs::insert_list).
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipStream_t sst, hipEvent_t fork,
-                            hipEvent_t scatter_after);
+                            hipEvent_t scatter_after, hipEvent_t after_scan = nullptr);
 // The early head's list (FoldArgs::longs): on a stream of its own, after the
 // prefix, beside the alias insert (both claim through the same table).
 hipError_t launch_fold_longs(const FoldArgs& a, int cus, hipStream_t st);

@@ -247,7 +247,7 @@ struct Device {
   // long chains runs on side_stream, forked from and joined to the caller's
   DevBuf f_table, f_rep, f_tmax, f_cnt, f_order, f_key, f_tkeys, f_longs;
   hipStream_t head_stream = nullptr;  // a folded call's early head (FoldArgs::longs)
-  hipEvent_t ev_longs = nullptr, ev_join2 = nullptr;
+  hipEvent_t ev_longs = nullptr, ev_join2 = nullptr, ev_hready = nullptr;
   uint32_t f_epoch = 0;  // the alias table's epoch tag of the last folded call (plan.hip fold_claim)
   DevBuf probe;  // msha_clock_probe: stamps + sink
   // direct path heads (launch_head): their digests, lane-indexed; read back with
@@ -286,7 +286,7 @@ struct Device {
       b->release();
     for (hipEvent_t* e : {&ev0, &ev1, &ev_up0, &ev_up1, &ev_k0, &ev_meta, &ev_plan, &ev_p0, &ev_p1, &slot_free[0],
                           &slot_free[1], &chunk_in, &ev_fork, &ev_fplan, &ev_join, &ev_fdone, &ev_head,
-                          &ev_longs, &ev_join2}) {
+                          &ev_longs, &ev_join2, &ev_hready}) {
       if (*e) (void)hipEventDestroy(*e);
       *e = nullptr;
     }
@@ -3006,25 +3006,34 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
     // pass beside the prefix): off by default (profiles/r06_call4/).
     // With the look-back there is no tile prefix to decide in: the gate always
     // decides (64 workgroups; MSHA_GATE_WGS).
-    fa.early_fork = early && (lookback || env_u64("MSHA_EARLY_FORK", 0) != 0);
+    // Round 6 (MSHA_INSERT_LIST): with the look-back, the insert's own claims list
+    // the early head and the scan decides it -- no gate or list pass beside the
+    // insert -- and no late head runs (FoldArgs::insert_list).
+    const bool insert_list = early && lookback && env_u64("MSHA_INSERT_LIST", 0) != 0;
+    fa.insert_list = insert_list;
+    fa.early_fork = early && !insert_list && (lookback || env_u64("MSHA_EARLY_FORK", 0) != 0);
     fa.longs_wgs = (uint32_t)env_u64("MSHA_LONGS_WGS", 0);
     fa.gate_wgs = (uint32_t)env_u64("MSHA_GATE_WGS", 0);
+    // Round 6 A/B (MSHA_EARLY_ONLY=1): the early head takes every distinct long
+    // payload whether or not its chain is the call's long pole -- on the eight-lane
+    // kernel when it is, the two-lane one when the lane kernel is (both launched, the
+    // list's last workgroup arms one) -- and no late head is launched: the scatter
+    // and the lane kernel follow on the caller's stream, without the side stream's
+    // two cross-queue hand-offs. Payloads the list cannot hold stay lanes.
+    const bool early_only = insert_list || (fa.early_fork && env_u64("MSHA_EARLY_ONLY", 0) != 0);
+    fa.early_only = early_only;
+    const bool late_head = head && !early_only;
     if (fa.early_fork) {
       HIPCHK(hipEventRecord(d.ev_longs, st));
       HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
     }
     HIPCHK(msha::launch_fold_prefix(fa, st));
-    if (early) {
-      // the list runs beside the tile prefix (forked) or after it, and beside the
-      // alias insert
-      if (!fa.early_fork) {
-        HIPCHK(hipEventRecord(d.ev_longs, st));
-        HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
-      }
-      HIPCHK(msha::launch_fold_longs(fa, d.cus, d.head_stream));
-      HIPCHK(hipEventRecord(d.ev_longs, d.head_stream));
+    // the early head's launches on its stream: after the list (k_fold_longs) or,
+    // listed by the insert, after the scan (its event recorded by launch_fold_plan,
+    // so these are queued after that call)
+    auto launch_early_head = [&]() {
       msha::LaneGate eg;
-      eg.head = fa.info + 4;
+      eg.head = early_only && eight_lane ? fa.info + 20 : fa.info + 4;
       eg.head_part = true;
       eg.two_lane = true;
       eg.eight_lane = eight_lane;
@@ -3033,9 +3042,41 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
                                        d.err.as<uint32_t>(), d.cus, MSHA_KERNEL_COOP, d.head_stream, nullptr,
                                        &ek, &eg));
       count_launch(ctx, nullptr, ek);
+      if (early_only && eight_lane) {  // the same list on the two-lane kernel when not the long pole
+        eg.head = fa.info + 21;
+        eg.eight_lane = false;
+        HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, fa.longs, nullptr, fa.long_cap, d_out,
+                                         d.err.as<uint32_t>(), d.cus, MSHA_KERNEL_COOP, d.head_stream, nullptr,
+                                         &ek, &eg));
+        count_launch(ctx, nullptr, ek);
+      }
       HIPCHK(hipEventRecord(d.ev_join2, d.head_stream));
+    };
+    if (early && !insert_list) {
+      // the list runs beside the tile prefix (forked) or after it, and beside the
+      // alias insert
+      if (!fa.early_fork) {
+        HIPCHK(hipEventRecord(d.ev_longs, st));
+        HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
+      }
+      HIPCHK(msha::launch_fold_longs(fa, d.cus, d.head_stream));
+      HIPCHK(hipEventRecord(d.ev_longs, d.head_stream));
+      launch_early_head();
     }
-    HIPCHK(msha::launch_fold_plan(fa, st, ps, d.ev_fork, early ? d.ev_longs : nullptr));
+    HIPCHK(msha::launch_fold_plan(fa, st, late_head ? ps : st, d.ev_fork,
+                                  early && !insert_list ? d.ev_longs : nullptr,
+                                  insert_list ? d.ev_longs : nullptr));
+    if (insert_list) {  // (ev_longs here: after the scan, on st)
+      HIPCHK(hipStreamWaitEvent(d.head_stream, d.ev_longs, 0));
+      // the lane kernel waits until the head's stream reaches its launches (an event
+      // recorded just before them): dispatched together, the lane kernel ran ~25 %
+      // more cycles a block (profiles/r06_il_stamps/); the wait overlaps the scatter
+      if (env_u64("MSHA_INSERT_LIST_SYNC", 1)) {
+        if (!d.ev_hready) HIPCHK(hipEventCreateWithFlags(&d.ev_hready, hipEventDisableTiming));
+        HIPCHK(hipEventRecord(d.ev_hready, d.head_stream));
+      }
+      launch_early_head();
+    }
     const uint32_t* order = d.f_order.as<uint32_t>();
     msha::LaunchKind kind;
     if (all_coop) {
@@ -3052,7 +3093,7 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
         body.ws_ctr = reinterpret_cast<uint32_t*>(fa.big + 2 * msha::kFoldBigBuckets);
         body.lanes = fa.info;
       }
-      if (head) {
+      if (late_head) {
         HIPCHK(hipEventRecord(d.ev_fplan, d.side_stream));
         msha::LaneGate hg;
         hg.head = fa.info + 5;  // the scan's cut (0 when the early head has the long lanes)
@@ -3065,10 +3106,11 @@ int msha_digest_batch_device_planned(msha_ctx* ctx, const uint8_t* d_arena, cons
         HIPCHK(hipEventRecord(d.ev_join, d.side_stream));
         HIPCHK(hipStreamWaitEvent(st, d.ev_fplan, 0));
       }
+      if (insert_list && env_u64("MSHA_INSERT_LIST_SYNC", 1)) HIPCHK(hipStreamWaitEvent(st, d.ev_hready, 0));
       HIPCHK(msha::launch_digest_batch(d_arena, d_off, d_len, order, nullptr, n, d_out, d.err.as<uint32_t>(),
                                        d.cus, ctx->kernel_policy, st, nullptr, &kind, &body));
       count_launch(ctx, nullptr, kind);
-      if (head) HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
+      if (late_head) HIPCHK(hipStreamWaitEvent(st, d.ev_join, 0));
       if (early) HIPCHK(hipStreamWaitEvent(st, d.ev_join2, 0));
     }
     if (fold) HIPCHK(msha::launch_fold_fill(fa, d_out, st));

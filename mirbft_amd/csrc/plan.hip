@@ -761,6 +761,12 @@ __global__ __launch_bounds__(256, 4) void k_fold_insert(FoldArgs a) {
       rp = fold_claim(a, i, a.off[i], ln);
       if (rp == (uint32_t)i) fold_hist_add(hist, ln);
       trep[trep_at(li)] = rp == (uint32_t)i ? (uint16_t)fold_key(ln) : (uint16_t)0xFFFFu;
+      // (insert_list) a long payload's claimant is the early head's: listed here, as
+      // k_fold_longs would (every long message is a candidate, so every long lane)
+      if (a.insert_list && rp == (uint32_t)i && dev_blocks_for(ln) >= a.long_blocks) {
+        const uint32_t k = atomicAdd(&a.info[2], 1u);
+        if (k < a.long_cap) a.longs[k] = (uint32_t)i;
+      }
     }
     const bool folded = c < nc && rp != (uint32_t)i;
     const uint64_t fm = __ballot(folded);
@@ -875,9 +881,10 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   __shared__ uint32_t w_cnt[16], w_min[16], w_h[16];
   __shared__ uint64_t w_blk[16], w_key[16];
   __shared__ uint32_t s_long;  // lanes of >= long_blocks blocks
+  __shared__ unsigned long long s_long_blocks;  // and their blocks
   PLAN_STAMP(kPsScan, 0);
   const uint32_t t = threadIdx.x, lane = __lane_id(), wave = t >> 6;
-  if (t == 0) s_long = 0;
+  if (t == 0) s_long = 0, s_long_blocks = 0;
   constexpr uint32_t per = (kFoldBuckets + 1023) / 1024;
   const uint32_t b0 = min(t * per, kFoldBuckets);
   uint32_t c[per];
@@ -926,7 +933,7 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
   for (uint32_t k = 0; k < per; ++k) {  // cut before bucket b: h = run, its longest = bucket b
     const uint32_t b = b0 + k;
     if (b >= kFoldBuckets) break;
-    if (b == klong) s_long = run;
+    if (b == klong) s_long = run, s_long_blocks = brun;
     if (c[k] && a.head_cap) {
       const uint64_t cost = head_cost(a, run, brun, btot, max_blocks, key_max_blocks(a, b));
       const uint64_t key = (min(cost, kCostMax) << 20) | b;
@@ -977,6 +984,18 @@ __global__ __launch_bounds__(1024) void k_fold_scan(FoldArgs a) {
     a.info[0] = lanes;
     a.info[16] = s_long;
     a.info[17] = late;
+    if (a.insert_list) {
+      // The early head listed by the insert: always (every distinct long payload the
+      // list holds), on the eight-lane kernel when its chain is the call's long pole
+      // -- the lanes' other blocks over the SIMDs take less -- else the two-lane one
+      const uint32_t c = a.info[2];
+      const uint64_t t_body = (btot - s_long_blocks) * a.wave_block_cycles / (64ull * a.simds);
+      const bool pole = t_body < max_blocks * a.early_cycles;
+      const uint32_t e = c <= a.long_cap ? c : 0u;
+      a.info[4] = e;
+      a.info[20] = pole ? e : 0u;
+      a.info[21] = pole ? 0u : e;
+    }
     PLAN_STAMP(kPsScan, 1);
   }
 }
@@ -1005,7 +1024,7 @@ __global__ __launch_bounds__(256) void k_fold_scatter(FoldArgs a) {
 #else  // round 5's committed rule, for the check's regression test (tools/r05_race.sh)
     const uint32_t early = a.long_blocks ? a.info[4] : 0u;
 #endif
-    const uint32_t late = a.info[17];
+    const uint32_t late = a.early_only ? 0u : a.info[17];  // (early_only: no late head)
     a.info[1] = early ? early : late;
     a.info[5] = early ? 0u : late;
   }
@@ -1153,7 +1172,15 @@ __global__ __launch_bounds__(256) void k_fold_longs(FoldArgs a) {
     const uint32_t c = __hip_atomic_load(&a.info[2], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t t_body = tot * a.wave_block_cycles / (64ull * a.simds);
     const uint64_t t_head = lng * a.early_cycles;
-    a.info[4] = c <= a.long_cap && t_body < t_head ? c : 0u;
+    const bool pole = t_body < t_head;  // the head's chain outlasts the lane kernel's share
+    if (a.early_only) {
+      const uint32_t e = c <= a.long_cap ? c : 0u;
+      a.info[4] = e;
+      a.info[20] = pole ? e : 0u;
+      a.info[21] = pole ? 0u : e;
+    } else {
+      a.info[4] = c <= a.long_cap && pole ? c : 0u;
+    }
   }
 }
 
@@ -1193,7 +1220,7 @@ __global__ __launch_bounds__(256) void k_fold_longs_gate(FoldArgs a) {
   if (threadIdx.x == 0 && grid_reduce_last(a.grid_ws + kGridWords, s_sum, s_max, ss, sm)) {
     const uint64_t t_body = ss * a.wave_block_cycles / (64ull * a.simds);
     const uint64_t t_head = sm * a.early_cycles;
-    a.info[6] = sm >= a.long_blocks && t_body < t_head ? 1u : 0u;
+    a.info[6] = sm >= a.long_blocks && (a.early_only || t_body < t_head) ? 1u : 0u;
   }
   PLAN_STAMP(kPsGate, 1);
 }
@@ -1250,13 +1277,17 @@ hipError_t launch_fold_prefix(const FoldArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_fold_plan(const FoldArgs& a, hipStream_t st, hipStream_t sst, hipEvent_t fork,
-                            hipEvent_t scatter_after) {
+                            hipEvent_t scatter_after, hipEvent_t after_scan) {
   if (a.n == 0) return hipSuccess;
   const unsigned ptiles = (unsigned)((a.n + kPlanTile - 1) / kPlanTile);
   if (a.table) hipLaunchKernelGGL(k_fold_insert, dim3(ptiles), dim3(256), 0, st, a);
   const unsigned ftiles = (unsigned)((a.n + kFoldTile - 1) / kFoldTile);
   if (!a.table) hipLaunchKernelGGL(k_fold_keys, dim3(ftiles), dim3(256), 0, st, a);
   hipLaunchKernelGGL(k_fold_scan, dim3(1), dim3(1024), 0, st, a);
+  if (after_scan) {
+    const hipError_t e = hipEventRecord(after_scan, st);
+    if (e != hipSuccess) return e;
+  }
   if (sst != st) {
     hipError_t e = hipEventRecord(fork, st);
     if (e == hipSuccess) e = hipStreamWaitEvent(sst, fork, 0);
